@@ -1,0 +1,381 @@
+#!/usr/bin/env python3
+"""Benchmark of the server-side aggregation hot path on MI355X.
+
+Headline (BASELINE.json ``metric``): client-update GB/s aggregated per FL round,
+on BASELINE config 2 — FedAvg of 100 synthetic ResNet-18 (11,173,962 fp32)
+client updates per GPU, bit-exact reference-order kernel.  One "step" = one
+aggregation of the resident client rows (plus, for N > 1 GPUs, the RCCL
+all-reduce of the partial sums; clients are sharded, K per rank: weak scaling).
+
+The same JSON line carries:
+  * ``roofline``     dominant kernel (dls_fedavg_f32): algorithmic bytes per
+                     launch / its average duration from HIP events recorded on
+                     the launch stream around every launch of the timed region;
+  * ``cpu_baseline`` the reference's own torch op sequence (oracle restatement,
+                     servers/fed_server.py:52-65) on this host's cores, bounded
+                     sample, rank 0 at N = 1 only;
+  * ``components``   the other BASELINE configs (sign vote 1000 x ResNet-18,
+                     fed_quant 100 x VGG-16, Shapley subset GEMM 50 x ResNet-18),
+                     each with its own roofline (skip with --quick).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--quick]
+"""
+import argparse
+import json
+import math
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from distributed_learning_simulator_amd import _native  # noqa: E402
+from distributed_learning_simulator_amd.layout import ParameterLayout  # noqa: E402
+from distributed_learning_simulator_amd.model_shapes import resnet18_cifar, vgg16  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
+SEED = 20250127
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def timed_launches(fn, steps, warmup, sync_all=None):
+    """Run fn() warmup+steps times; HIP events around every timed launch on the
+    current stream.  Returns (wall_s, [kernel_ms...])."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if sync_all:
+        sync_all()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        fn(a, b)
+    torch.cuda.synchronize()
+    if sync_all:
+        sync_all()
+    wall = time.perf_counter() - t0
+    return wall, [a.elapsed_time(b) for a, b in ev]
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def roofline(kernel, bytes_per_launch, kernel_ms, bound="hbm", flops_per_launch=None):
+    avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    if bound == "hbm":
+        achieved = bytes_per_launch / avg_s / 1e9
+        peak, unit = HBM_PEAK_GBS, "GB/s"
+    else:
+        achieved = flops_per_launch / avg_s / 1e12
+        peak, unit = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
+    return {"kernel": kernel, "bound": bound, "achieved": round(achieved, 2), "peak": peak,
+            "unit": unit, "frac": round(achieved / peak, 4), "traffic": load_traffic(kernel),
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "avg_launch_us": round(avg_s * 1e6, 2)}
+
+
+def synth_updates(K, P, dev, seed):
+    """U_i = base + sigma_i * N(0,1), base ~ N(0, 0.05^2),
+    sigma_i log-uniform in [1e-3, 5e-2], n_i ~ U{100..1000}."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    U = torch.empty((K, P), dtype=torch.float32, device=dev)
+    U.normal_(generator=g)
+    base = torch.randn(P, generator=g, device=dev) * 0.05
+    lo, hi = math.log(1e-3), math.log(5e-2)
+    sig = torch.exp(lo + (hi - lo) * torch.rand(K, generator=g, device=dev))
+    U.mul_(sig[:, None]).add_(base[None, :])
+    n = torch.randint(100, 1001, (K,), generator=g, device=dev).tolist()
+    return U, n
+
+
+# ----------------------------------------------------------------- FedAvg
+def bench_fedavg(args, dev, rank, world):
+    layout = ParameterLayout(resnet18_cifar())
+    P, K = layout.P, args.clients
+    U, n = synth_updates(K, P, dev, SEED + 1 + rank)
+    # global sample count (FedAvg over all ranks' clients)
+    n_all = torch.tensor([sum(n)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(n_all)
+    total = float(n_all.item())
+    rows = torch.arange(K, dtype=torch.int32, device=dev)
+    w = torch.tensor(n, dtype=torch.float32, device=dev)
+    out = torch.empty(P, dtype=torch.float32, device=dev)
+    chunks = args.chunks if world > 1 else 1
+    bounds = [P * c // chunks // 256 * 256 for c in range(chunks)] + [P]
+    kms = []
+
+    def step(a=None, b=None):
+        handles = []
+        for c in range(chunks):
+            c0, c1 = bounds[c], bounds[c + 1]
+            if a is not None and c == 0:
+                a.record()
+            _native.fedavg(U[:, c0:], rows, w, total, c1 - c0, out[c0:c1])
+            if b is not None and c == chunks - 1:
+                b.record()
+            if world > 1:
+                handles.append(dist.all_reduce(out[c0:c1], async_op=True))
+        for h in handles:
+            h.wait()
+
+    sync_all = dist.barrier if world > 1 else None
+    wall, kms = timed_launches(step, args.steps, args.warmup, sync_all)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    ms = wall / args.steps * 1e3
+    upd_bytes = layout.numel * 4  # one client update (fp32, unpadded)
+    value = world * K * upd_bytes / (ms / 1e3) / 1e9
+    bytes_per_launch = K * P * 4 + P * 4
+    rf = roofline("dls_fedavg_f32", bytes_per_launch, kms)
+    if world > 1:  # the events bracket all chunks' kernels (and interleaved RCCL enqueue)
+        rf["note"] = "launch window includes chunked all-reduce overlap"
+    del U
+    return value, ms, rf, {"clients_per_gpu": K, "params": layout.numel, "padded_row": P}
+
+
+# ------------------------------------------------------------ components
+def bench_sign(args, dev):
+    layout = ParameterLayout(resnet18_cifar())
+    P, K = layout.P, 1000
+    W = _native.sign_words(P)
+    g = torch.Generator(device=dev).manual_seed(SEED + 3)
+    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]
+    sign_out = torch.empty(P, device=dev)
+    counts = torch.empty(P, dtype=torch.int32, device=dev)
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.sign_vote(planes, None, K, P, sign_out, counts)
+        if b is not None:
+            b.record()
+
+    wall, kms = timed_launches(step, args.steps, args.warmup)
+    ms = wall / args.steps * 1e3
+    wire = W * 8
+    bytes_per_launch = K * wire + 2 * P * 4
+    # worker/server pack kernel: fp32 signs -> planes, 16 clients per launch
+    X = torch.sign(torch.randn((16, P), generator=g, device=dev))
+    pk = torch.empty((16, W), dtype=torch.int64, device=dev)
+
+    def pstep(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.sign_pack(X, P, pk)
+        if b is not None:
+            b.record()
+
+    _, pkms = timed_launches(pstep, args.steps, args.warmup)
+    del planes, X
+    return {
+        "config": "signSGD majority vote, 1000 clients x ResNet-18 (2-bit planes)",
+        "value": round(K * wire / (ms / 1e3) / 1e9, 2), "unit": "GB/s (packed client updates)",
+        "fp32_logical_GBps": round(K * layout.numel * 4 / (ms / 1e3) / 1e9, 2),
+        "ms_per_step": round(ms, 4), "roofline": roofline("dls_sign_vote", bytes_per_launch, kms),
+        "pack": roofline("dls_sign_pack_f32", 16 * (P * 4 + W * 8), pkms),
+    }
+
+
+def bench_quant(args, dev):
+    from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
+    shapes = vgg16()
+    K = 100
+    template = {}
+    for name, s in shapes:
+        if len(s) >= 2:
+            template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
+                              torch.zeros(s[0], dtype=torch.int64))
+        else:
+            template[name] = torch.zeros(s)
+    store = QuantizedClientStore(template, dev, capacity=K)
+    g = torch.Generator(device=dev).manual_seed(SEED + 4)
+    store.Q.random_(0, 256, generator=g)  # int8 payload bytes
+    store.F.normal_(generator=g).mul_(0.01)
+    store.sz[:, :, 0].uniform_(1e-4, 1e-2, generator=g)
+    store.sz[:, :, 1].zero_()
+    rows = list(range(K))
+    store._free = []
+    n = torch.randint(100, 1001, (K,), generator=g).tolist()
+    out = torch.empty(store.layout.P, device=dev)
+    rows_t = torch.tensor(rows, dtype=torch.int32, device=dev)
+    w_t = torch.tensor(n, dtype=torch.float32, device=dev)
+    total = float(sum(n))
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.dequant_fedavg(store.tiles, store.ntiles, store.Q, store.F, store.sz, rows_t, w_t,
+                               total, out)
+        if b is not None:
+            b.record()
+
+    wall, kms = timed_launches(step, args.steps, args.warmup)
+    ms = wall / args.steps * 1e3
+    ql = store.qlayout
+    Pq = sum(m for m, k in zip(store.layout.numels, ql.kinds) if k)
+    Pf = sum(m for m, k in zip(store.layout.numels, ql.kinds) if not k)
+    client_bytes = Pq + 4 * Pf + 8 * ql.C
+    bytes_per_launch = K * client_bytes + 4 * store.layout.numel
+    del store
+    return {
+        "config": "fed_quant 8-bit, 100 clients x VGG-16, fused dequant + FedAvg (bit-exact)",
+        "value": round(K * client_bytes / (ms / 1e3) / 1e9, 2),
+        "unit": "GB/s (int8 client updates)",
+        "fp32_logical_GBps": round(K * (Pq + Pf) * 4 / (ms / 1e3) / 1e9, 2),
+        "ms_per_step": round(ms, 4),
+        "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms),
+    }
+
+
+def bench_shapley_gemm(args, dev):
+    layout = ParameterLayout(resnet18_cifar())
+    P, K, S = layout.P, 50, args.subsets
+    U, n = synth_updates(K, P, dev, SEED + 5)
+    g = torch.Generator().manual_seed(SEED + 5)
+    member = torch.rand((S, K), generator=g) < 0.5
+    member[:, 0] = True
+    nn_ = torch.tensor(n, dtype=torch.float64)
+    C = (member.double() * nn_[None, :])
+    C = (C / C.sum(1, keepdim=True)).float().to(dev)
+    rows = torch.arange(K, dtype=torch.int32, device=dev)
+    out = torch.empty((S, P), device=dev)
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.subset_gemm(C, U, rows, P, out)
+        if b is not None:
+            b.record()
+
+    wall, kms = timed_launches(step, args.steps, args.warmup)
+    ms = wall / args.steps * 1e3
+    flops = 2.0 * S * K * layout.numel
+    bytes_per_launch = (K + S) * P * 4
+    rf_hbm = roofline("dls_subset_gemm_f32", bytes_per_launch, kms)
+    rf_mfma = roofline("dls_subset_gemm_f32", bytes_per_launch, kms, bound="mfma",
+                       flops_per_launch=flops)
+    del U, out
+    return {
+        "config": f"Shapley subset aggregation as fp32 MFMA GEMM, {S} subsets x 50 clients x ResNet-18",
+        "value": round(S / (ms / 1e3), 1), "unit": "subset models/s",
+        "ms_per_step": round(ms, 4), "roofline": rf_hbm, "mfma": rf_mfma,
+    }
+
+
+# ---------------------------------------------------------- CPU baseline
+def cpu_baseline(args):
+    """Reference torch op sequence (servers/fed_server.py:52-65) on the host CPU."""
+    from oracle.fedavg import fedavg_torch_cpu  # test infrastructure, timed only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(threads)
+    shapes = resnet18_cifar()
+    Kc = args.cpu_clients
+    g = torch.Generator().manual_seed(SEED)
+    clients = [{k: torch.randn(s, generator=g) * 0.05 for k, s in shapes} for _ in range(Kc)]
+    n = [100 + 9 * i for i in range(Kc)]
+    order = list(range(Kc))
+    fedavg_torch_cpu(clients, n, order)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fedavg_torch_cpu(clients, n, order)
+        reps += 1
+        el = time.perf_counter() - t0
+        if (el >= args.cpu_seconds and reps >= 2) or el >= 3 * args.cpu_seconds:
+            break
+    per = el / reps
+    P = sum(math.prod(s) for _, s in shapes)
+    model = ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
+                      if l.startswith("Model name")), "")
+    except Exception:
+        pass
+    return {"value": round(Kc * P * 4 / per / 1e9, 3), "unit": "GB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{Kc} ResNet-18 client dicts (fp32, 62 tensors), reference torch op "
+                      f"sequence, {reps} reps in {el:.1f}s",
+            "cpu_model": model or platform.processor(), "ms_per_aggregation": round(per * 1e3, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--clients", type=int, default=100, help="client updates per GPU")
+    ap.add_argument("--chunks", type=int, default=4, help="all-reduce pipeline chunks (N>1)")
+    ap.add_argument("--subsets", type=int, default=50)
+    ap.add_argument("--quick", action="store_true", help="headline only (no components)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-clients", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    _native.require_gpu()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    value, ms, rf, extra = bench_fedavg(args, dev, rank, world)
+    components = {}
+    if not args.quick and rank == 0:
+        for name, fn in (("sign_vote", bench_sign), ("fed_quant", bench_quant),
+                         ("shapley_gemm", bench_shapley_gemm)):
+            try:
+                components[name] = fn(args, dev)
+                log(name, json.dumps(components[name]))
+            except Exception as e:  # report, never hide
+                components[name] = {"error": repr(e)}
+            torch.cuda.empty_cache()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        line = {
+            "metric": "client-update GB/s aggregated per FL round",
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "FedAvg aggregation of 100 synthetic ResNet-18 (11.2M-param "
+                                   "fp32) client updates per GPU, bit-exact reference order",
+                       "parallelism": f"clients sharded over {world} GPU(s) + RCCL all-reduce",
+                       **extra},
+            "roofline": rf, "cpu_baseline": cpu, "components": components,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+"""ctypes binding of libdls_hip.so (the C-ABI declared in include/dls_hip.h).
+
+Every wrapper takes torch tensors that already live on the current HIP device,
+passes raw pointers and the current stream to the library, and raises
+``RuntimeError`` (with ``dls_last_error()``) on a non-zero status.  There is no
+CPU or PyTorch fallback: if the library cannot be loaded, or a tensor is not on
+the GPU, the call fails loudly.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DLS_HIP_LIB", os.path.join(_HERE, "libdls_hip.so"))
+
+FEDAVG_EXACT = 0
+FEDAVG_FMA = 1
+SIGN_NAN_MARK = 1 << 24
+
+
+def sign_words(P):
+    """uint64 words per client row of sign planes (DLS_SIGN_WORDS)."""
+    return ((P + 255) // 256) * 8
+
+
+class QTile(ctypes.Structure):
+    """struct dls_qtile (include/dls_hip.h)."""
+
+    _fields_ = [
+        ("dst", ctypes.c_int64),
+        ("src", ctypes.c_int64),
+        ("len", ctypes.c_int32),
+        ("kind", ctypes.c_int32),
+        ("chan0", ctypes.c_int32),
+        ("row_len", ctypes.c_int32),
+        ("row_pos", ctypes.c_int32),
+        ("chan_end", ctypes.c_int32),
+    ]
+
+
+_i32, _i64, _f32, _p, _u64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p,
+                              ctypes.c_uint64)
+
+# name -> argtypes (restype int unless noted); mirrors include/dls_hip.h
+SIGNATURES = {
+    "dls_last_error": ([], ctypes.c_char_p),
+    "dls_abi_version": ([], _i32),
+    "dls_device_count": ([], _i32),
+    "dls_fedavg_f32": ([_p, _i64, _p, _p, _i32, _f32, _i64, _i32, _p, _p], _i32),
+    "dls_subset_fedavg_f32": ([_p, _i64, _p, _p, _p, _p, _i32, _i64, _p, _i64, _p], _i32),
+    "dls_subset_gemm_f32": ([_p, _i32, _i32, _p, _i64, _p, _i64, _p, _i64, _p], _i32),
+    "dls_sign_pack_f32": ([_p, _i64, _i32, _i64, _p, _i64, _p, _p], _i32),
+    "dls_sign_vote_count": ([_p, _i64, _p, _i32, _i64, _p, _p], _i32),
+    "dls_sign_from_counts": ([_p, _i64, _p, _p, _p], _i32),
+    "dls_sign_vote": ([_p, _i64, _p, _i32, _i64, _p, _p, _p], _i32),
+    "dls_sign_sgd_direction": ([_p, _p, _i64, _f32, _f32, _i32, _i32, _p, _p, _p], _i32),
+    "dls_sign_sgd_apply": ([_p, _p, _i64, _f32, _f32, _p], _i32),
+    "dls_dequant_fedavg": ([_p, _i32, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i32, _f32, _p, _p],
+                           _i32),
+    "dls_segment_minmax_f32": ([_p, _p, _i32, _p, _p, _i64, _p], _i32),
+    "dls_qparams_minmax": ([_p, _p, _i32, _i32, _i32, _p, _p, _p], _i32),
+    "dls_quantize_u8": ([_p, _p, _i32, _p, _p, _p, _p, _i32, _u64, _i64, _p], _i32),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libdls_hip.so once (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"libdls_hip.so not found at {LIB_PATH}; build it with "
+                        "`make -C distributed_learning_simulator_amd/csrc` (no CPU fallback)")
+                L = ctypes.CDLL(LIB_PATH)
+                for name, (args, res) in SIGNATURES.items():
+                    f = getattr(L, name)
+                    f.argtypes = args
+                    f.restype = res
+                _lib = L
+    return _lib
+
+
+def _check(rc, name):
+    if rc != 0:
+        msg = lib().dls_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("libdls_hip: tensor is not on the GPU (no CPU fallback)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("distributed_learning_simulator_amd needs a ROCm GPU (no CPU fallback)")
+    lib()
+
+
+# ---------------------------------------------------------------------- FedAvg
+def fedavg(U, rows, weight, total, P, out, mode=FEDAVG_EXACT, stream=None):
+    """servers/fed_server.py:44-66 over rows of U (see dls_fedavg_f32)."""
+    assert U.dtype == torch.float32 and out.dtype == torch.float32
+    assert rows.dtype == torch.int32 and weight.dtype == torch.float32
+    _check(lib().dls_fedavg_f32(_ptr(U), U.stride(0), _ptr(rows), _ptr(weight), rows.numel(),
+                                float(total), P, mode, _ptr(out), _stream(stream)),
+           "dls_fedavg_f32")
+    return out
+
+
+def subset_fedavg(U, sub_off, sub_rows, sub_weight, sub_total, P, out, stream=None):
+    S = sub_off.numel() - 1
+    _check(lib().dls_subset_fedavg_f32(_ptr(U), U.stride(0), _ptr(sub_off), _ptr(sub_rows),
+                                       _ptr(sub_weight), _ptr(sub_total), S, P, _ptr(out),
+                                       out.stride(0), _stream(stream)), "dls_subset_fedavg_f32")
+    return out
+
+
+def subset_gemm(C, U, rows, P, out, stream=None):
+    S, K = C.shape
+    assert C.is_contiguous() and C.dtype == torch.float32
+    _check(lib().dls_subset_gemm_f32(_ptr(C), S, K, _ptr(U), U.stride(0), _ptr(rows), P, _ptr(out),
+                                     out.stride(0), _stream(stream)), "dls_subset_gemm_f32")
+    return out
+
+
+# ------------------------------------------------------------------------ sign
+def sign_pack(X, P, planes, nonternary=None, stream=None):
+    K = X.shape[0]
+    _check(lib().dls_sign_pack_f32(_ptr(X), X.stride(0), K, P, _ptr(planes), planes.stride(0),
+                                   _ptr(nonternary), _stream(stream)), "dls_sign_pack_f32")
+    return planes
+
+
+def sign_vote_count(planes, rows, K, P, counts, stream=None):
+    _check(lib().dls_sign_vote_count(_ptr(planes), planes.stride(0), _ptr(rows), K, P,
+                                     _ptr(counts), _stream(stream)), "dls_sign_vote_count")
+    return counts
+
+
+def sign_from_counts(counts, P, sign_out=None, vote_planes=None, stream=None):
+    _check(lib().dls_sign_from_counts(_ptr(counts), P, _ptr(sign_out), _ptr(vote_planes),
+                                      _stream(stream)), "dls_sign_from_counts")
+
+
+def sign_vote(planes, rows, K, P, sign_out, counts=None, stream=None):
+    _check(lib().dls_sign_vote(_ptr(planes), planes.stride(0), _ptr(rows), K, P, _ptr(counts),
+                               _ptr(sign_out), _stream(stream)), "dls_sign_vote")
+    return sign_out
+
+
+def sign_sgd_direction(grad, buf, momentum, one_minus_dampening, nesterov, first, planes,
+                       sign_out=None, stream=None):
+    P = grad.numel()
+    _check(lib().dls_sign_sgd_direction(_ptr(grad), _ptr(buf), P, float(momentum),
+                                        float(one_minus_dampening), int(bool(nesterov)),
+                                        int(bool(first)), _ptr(planes), _ptr(sign_out),
+                                        _stream(stream)), "dls_sign_sgd_direction")
+
+
+def sign_sgd_apply(param, vote_planes, neg_lr, weight_decay, stream=None):
+    _check(lib().dls_sign_sgd_apply(_ptr(param), _ptr(vote_planes), param.numel(), float(neg_lr),
+                                    float(weight_decay), _stream(stream)), "dls_sign_sgd_apply")
+
+
+# ----------------------------------------------------------------------- quant
+def dequant_fedavg(tiles, ntiles, Q, F, sz, rows, weight, total, out, stream=None):
+    _check(lib().dls_dequant_fedavg(_ptr(tiles), ntiles, _ptr(Q), Q.stride(0) if Q is not None else 0,
+                                    _ptr(F), F.stride(0) if F is not None else 0, _ptr(sz),
+                                    sz.stride(0) // 2, _ptr(rows),
+                                    _ptr(weight), rows.numel(), float(total), _ptr(out),
+                                    _stream(stream)), "dls_dequant_fedavg")
+    return out
+
+
+def segment_minmax(x, seg_off, total, mins, maxs, stream=None):
+    _check(lib().dls_segment_minmax_f32(_ptr(x), _ptr(seg_off), seg_off.numel() - 1, _ptr(mins),
+                                        _ptr(maxs), total, _stream(stream)),
+           "dls_segment_minmax_f32")
+
+
+def qparams_minmax(mins, maxs, scale, zp, qmin=0, qmax=255, stream=None):
+    _check(lib().dls_qparams_minmax(_ptr(mins), _ptr(maxs), mins.numel(), qmin, qmax, _ptr(scale),
+                                    _ptr(zp), _stream(stream)), "dls_qparams_minmax")
+
+
+def quantize_u8(x, seg_off, total, scale, zp, q, deq=None, stochastic=False, seed=0,
+                stream=None):
+    _check(lib().dls_quantize_u8(_ptr(x), _ptr(seg_off), seg_off.numel() - 1, _ptr(scale),
+                                 _ptr(zp), _ptr(q), _ptr(deq), int(bool(stochastic)),
+                                 ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), total,
+                                 _stream(stream)), "dls_quantize_u8")

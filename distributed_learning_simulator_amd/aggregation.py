@@ -1,0 +1,172 @@
+"""Device-resident client-update stores and the aggregation calls on them.
+
+HBM layout:
+
+* ``ClientUpdateStore.U``  fp32 [capacity, P]: one row per client, the flat
+  parameter layout of ``layout.ParameterLayout`` (tensors in dict order, each
+  64-element aligned).  A FedAvg round is one ``dls_fedavg_f32`` launch over K
+  rows: K*P*4 bytes read once, P*4 written.
+* ``ClientParameters`` keeps the reference's ``self.parameters`` mapping
+  (servers/fed_server.py:15,69-73,87) — ``{worker_id: (n_i, dict)}`` in arrival
+  order — but the dict values are views of the client's row in ``U``, so the
+  reference hooks and user code still see per-tensor dicts.
+"""
+import threading
+
+import torch
+
+from . import _native
+from .layout import ParameterLayout
+
+
+def _i32(xs, device):
+    return torch.tensor(list(xs), dtype=torch.int32).to(device, non_blocking=True)
+
+
+def _f32(xs, device):
+    return torch.tensor(list(xs), dtype=torch.float32).to(device, non_blocking=True)
+
+
+class ClientUpdateStore:
+    def __init__(self, layout: ParameterLayout, device, capacity=1):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.U = torch.zeros((max(1, capacity), layout.P), dtype=torch.float32, device=self.device)
+        self._free = list(range(self.U.shape[0]))[::-1]
+        self._lock = threading.Lock()
+
+    @property
+    def capacity(self):
+        return self.U.shape[0]
+
+    def acquire(self):
+        with self._lock:
+            if not self._free:
+                old = self.U
+                new_cap = max(2 * old.shape[0], 1)
+                self.U = torch.zeros((new_cap, self.layout.P), dtype=torch.float32,
+                                     device=self.device)
+                self.U[: old.shape[0]].copy_(old)
+                self._free = list(range(old.shape[0], new_cap))[::-1]
+            return self._free.pop()
+
+    def release(self, row):
+        with self._lock:
+            self._free.append(row)
+
+    def write(self, row, parameter_dict):
+        self.layout.copy_into(parameter_dict, self.U[row])
+
+    def accepts(self, parameter_dict):
+        return self.layout.matches(parameter_dict)
+
+    def row(self, row):
+        return self.U[row]
+
+    def views(self, row):
+        return self.layout.views(self.U[row])
+
+    # ------------------------------------------------------------ aggregation
+    def fedavg(self, rows, ns, mode=_native.FEDAVG_EXACT, out=None):
+        """Weighted mean of rows in the given order (servers/fed_server.py:44-66)."""
+        P = self.layout.P
+        if out is None:
+            out = torch.empty(P, dtype=torch.float32, device=self.device)
+        total = sum(int(n) for n in ns)
+        _native.fedavg(self.U, _i32(rows, self.device), _f32([int(n) for n in ns], self.device),
+                       float(total), P, out, mode=mode)
+        return out
+
+    def subset_models(self, subsets, n_of_row, method="exact", out=None):
+        """S subset models at once.  subsets: list of row lists (non-empty, in order)."""
+        S = len(subsets)
+        P = self.layout.P
+        if out is None:
+            out = torch.empty((S, P), dtype=torch.float32, device=self.device)
+        if method == "exact":
+            off, flat_rows, flat_w, totals = [0], [], [], []
+            for sub in subsets:
+                flat_rows.extend(sub)
+                ws = [int(n_of_row[r]) for r in sub]
+                flat_w.extend(ws)
+                totals.append(float(sum(ws)))
+                off.append(len(flat_rows))
+            _native.subset_fedavg(self.U, _i32(off, self.device), _i32(flat_rows, self.device),
+                                  _f32(flat_w, self.device), _f32(totals, self.device), P, out)
+        elif method == "gemm":
+            rows = sorted({r for sub in subsets for r in sub})
+            col = {r: j for j, r in enumerate(rows)}
+            C = torch.zeros((S, len(rows)), dtype=torch.float64)
+            for s, sub in enumerate(subsets):
+                tot = float(sum(int(n_of_row[r]) for r in sub))
+                for r in sub:
+                    C[s, col[r]] = int(n_of_row[r]) / tot
+            _native.subset_gemm(C.float().to(self.device), self.U, _i32(rows, self.device), P, out)
+        else:
+            raise ValueError(f"unknown subset method {method!r}")
+        return out
+
+
+class ClientParameters(dict):
+    """``self.parameters`` of the reference FedServer, backed by a ClientUpdateStore.
+
+    ``params[worker_id] = (n, parameter_dict)`` copies the dict into the
+    worker's row; ``params[worker_id]`` returns ``(n, dict of row views)``.
+    """
+
+    def __init__(self, store_factory):
+        """store_factory(first_payload) -> store with acquire/release/write/views/accepts."""
+        super().__init__()
+        self._store_factory = store_factory
+        self.store = None
+        self._rows = {}
+
+    def _ensure_store(self, parameter_dict):
+        if self.store is None:
+            self.store = self._store_factory(parameter_dict)
+        elif not self.store.accepts(parameter_dict):
+            raise ValueError("client parameter dict does not match the model layout")
+
+    def __setitem__(self, worker_id, value):
+        n, parameter_dict = value
+        self._ensure_store(parameter_dict)
+        row = self._rows.get(worker_id)
+        if row is None:
+            row = self.store.acquire()
+            self._rows[worker_id] = row
+        self.store.write(row, parameter_dict)
+        super().__setitem__(worker_id, int(n))
+
+    def __getitem__(self, worker_id):
+        n = super().__getitem__(worker_id)
+        return n, self.store.views(self._rows[worker_id])
+
+    def __delitem__(self, worker_id):
+        super().__delitem__(worker_id)
+        self.store.release(self._rows.pop(worker_id))
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+    def pop(self, worker_id, *default):
+        if worker_id not in self and default:
+            return default[0]
+        v = self[worker_id]
+        del self[worker_id]
+        return v
+
+    def clear(self):
+        for k in list(self.keys()):
+            del self[k]
+
+    def row_of(self, worker_id):
+        return self._rows[worker_id]
+
+    def n_of(self, worker_id):
+        return dict.__getitem__(self, worker_id)
+
+    def n_of_row(self):
+        return {r: dict.__getitem__(self, w) for w, r in self._rows.items()}

@@ -1,0 +1,101 @@
+// Shared device/host helpers for libdls_hip.so (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/dls_hip.h"
+
+namespace dls {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------------ errors
+void set_error(const char *fmt, ...);
+
+#define DLS_REQUIRE(cond, code, ...)        \
+    do {                                    \
+        if (!(cond)) {                      \
+            ::dls::set_error(__VA_ARGS__);  \
+            return (code);                  \
+        }                                   \
+    } while (0)
+
+// Launch-error check after a hipLaunchKernelGGL (asynchronous errors surface
+// at the caller's next synchronisation).
+int check_launch(const char *what);
+
+inline hipStream_t as_stream(dls_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// --------------------------------------------------------- exact fp32 division
+// The reference divides fl32(p*n) by fl32(N) (servers/fed_server.py:59-60) with
+// one IEEE rounding.  On gfx950 the compiler's correctly rounded division is a
+// ~10-instruction v_div_scale/v_rcp/v_fma/v_div_fmas/v_div_fixup sequence; the
+// streaming kernels instead use Markstein's correction with y = RN(1/b):
+//     q0 = a*y ; r = fma(-q0, b, a) ; q = fma(r, y, q0)
+// which equals RN(a/b) whenever a, b and every intermediate stay in the normal
+// range.  Floating-point ops are scale-invariant there, so checking every fp32
+// mantissa of a in [1,2) proves it for one b; tests/test_oracle_golden.py does
+// that exhaustively for adversarial divisors (and 6,000+ more were checked while
+// building).  The kernels take the fast path for 2^-60 <= |a| <= 2^60 and
+// 1 <= b <= 2^31 (host side: `fast`) and fall back to IEEE `/` otherwise
+// (zeros incl. -0, denormals, inf, nan, huge values).
+struct FastDiv {
+    float b;
+    float y;
+    int fast;
+};
+
+inline FastDiv make_fastdiv(float b) {
+    FastDiv d;
+    d.b = b;
+    d.y = (float)(1.0 / (double)b);  // RN(1/b): double rounding is innocuous for '/'
+    d.fast = (b >= 1.0f && b <= 2147483648.0f) ? 1 : 0;
+    return d;
+}
+
+__device__ __forceinline__ float markstein(float a, float b, float y) {
+    const float q0 = a * y;
+    const float r = __builtin_fmaf(-q0, b, a);
+    return __builtin_fmaf(r, y, q0);
+}
+
+// 1 if 2^-60 <= |a| <= 2^60 (fast path valid), else 0.  Two VALU ops.
+__device__ __forceinline__ bool in_fast_range(float a) {
+    const uint32_t e = (__float_as_uint(a) >> 23) & 0xffu;  // biased exponent
+    return (e - (127u - 60u)) <= 120u;
+}
+
+// Division with the rare-path fix-up hoisted out of the common case: returns
+// false when the caller must redo the element with IEEE division.
+__device__ __forceinline__ float div_fast(float a, const FastDiv &d) {
+    return markstein(a, d.b, d.y);
+}
+
+__device__ __forceinline__ float div_ieee(float a, float b) {
+    return a / b;  // hipcc default: correctly rounded fp32 division
+}
+
+// Guarded exact division (one element).
+__device__ __forceinline__ float div_exact(float a, const FastDiv &d) {
+    if (d.fast && in_fast_range(a)) return markstein(a, d.b, d.y);
+    return a / d.b;
+}
+
+// ------------------------------------------------------------- misc device
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T ldg_nt(const T *p) {
+    return __builtin_nontemporal_load(p);
+}
+
+}  // namespace dls

@@ -1,0 +1,192 @@
+// FedAvg streaming reduction (servers/fed_server.py:44-66) for gfx950.
+//
+// One pass over the client rows: each lane owns 4 consecutive parameters
+// (one 16-byte load per client), walks the K clients in the reference's
+// iteration order and keeps the running sum in registers, so every client byte
+// is read once and the 4*P-byte result is written once.  HBM-bound: the
+// algorithmic traffic of one call is K*P*4 + P*4 bytes.
+//
+// EXACT mode reproduces the reference op sequence bit-for-bit:
+//     term_i = fl(fl(x * fl32(n_i)) / fl32(N)); acc = term_0; acc = fl(acc + term_i)
+// (division: dls_common.h, Markstein fast path + IEEE fix-up for out-of-range).
+// FMA mode computes acc = fma(x, fl(n_i/N), acc) (normwise ~1e-7).
+#include "dls_common.h"
+
+namespace dls {
+namespace {
+
+constexpr int kBlock = 256;
+
+template <bool NT>
+__device__ __forceinline__ f32x4 load4(const f32x4 *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+// term = fl(fl(x*w)/N) for 4 lanes of a f32x4, exact.
+__device__ __forceinline__ f32x4 term4(f32x4 x, float w, const FastDiv &d) {
+    f32x4 t;
+    t.x = x.x * w;
+    t.y = x.y * w;
+    t.z = x.z * w;
+    t.w = x.w * w;
+    f32x4 q;
+    q.x = markstein(t.x, d.b, d.y);
+    q.y = markstein(t.y, d.b, d.y);
+    q.z = markstein(t.z, d.b, d.y);
+    q.w = markstein(t.w, d.b, d.y);
+    const bool ok = d.fast & in_fast_range(t.x) & in_fast_range(t.y) & in_fast_range(t.z) &
+                    in_fast_range(t.w);
+    if (__builtin_expect(!ok, 0)) {  // zeros, denormals, huge, inf/nan: IEEE division
+        q.x = d.fast && in_fast_range(t.x) ? q.x : t.x / d.b;
+        q.y = d.fast && in_fast_range(t.y) ? q.y : t.y / d.b;
+        q.z = d.fast && in_fast_range(t.z) ? q.z : t.z / d.b;
+        q.w = d.fast && in_fast_range(t.w) ? q.w : t.w / d.b;
+    }
+    return q;
+}
+
+__device__ __forceinline__ f32x4 add4(f32x4 a, f32x4 b) {
+    return a + b;
+}
+
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(kBlock) void k_fedavg_exact(const f32x4 *__restrict__ U,
+                                                         int64_t ldu4,
+                                                         const int32_t *__restrict__ rows,
+                                                         const float *__restrict__ w, int K,
+                                                         FastDiv d, int64_t P4,
+                                                         f32x4 *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P4) return;
+    f32x4 acc = term4(load4<NT>(U + (int64_t)rows[0] * ldu4 + i), w[0], d);
+    int j = 1;
+    for (; j + UNROLL <= K; j += UNROLL) {
+        f32x4 x[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = load4<NT>(U + (int64_t)rows[j + u] * ldu4 + i);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc = add4(acc, term4(x[u], w[j + u], d));
+    }
+    for (; j < K; ++j) acc = add4(acc, term4(load4<NT>(U + (int64_t)rows[j] * ldu4 + i), w[j], d));
+    out[i] = acc;
+}
+
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(kBlock) void k_fedavg_fma(const f32x4 *__restrict__ U, int64_t ldu4,
+                                                       const int32_t *__restrict__ rows,
+                                                       const float *__restrict__ w, int K,
+                                                       float total, int64_t P4,
+                                                       f32x4 *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P4) return;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    int j = 0;
+    for (; j + UNROLL <= K; j += UNROLL) {
+        f32x4 x[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = load4<NT>(U + (int64_t)rows[j + u] * ldu4 + i);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const float c = w[j + u] / total;
+            acc.x = __builtin_fmaf(x[u].x, c, acc.x);
+            acc.y = __builtin_fmaf(x[u].y, c, acc.y);
+            acc.z = __builtin_fmaf(x[u].z, c, acc.z);
+            acc.w = __builtin_fmaf(x[u].w, c, acc.w);
+        }
+    }
+    for (; j < K; ++j) {
+        const f32x4 x = load4<NT>(U + (int64_t)rows[j] * ldu4 + i);
+        const float c = w[j] / total;
+        acc.x = __builtin_fmaf(x.x, c, acc.x);
+        acc.y = __builtin_fmaf(x.y, c, acc.y);
+        acc.z = __builtin_fmaf(x.z, c, acc.z);
+        acc.w = __builtin_fmaf(x.w, c, acc.w);
+    }
+    out[i] = acc;
+}
+
+// Batched reference-order subsets: blockIdx.y = subset.  Subsets of one GTG
+// wave / multiround batch share client rows, which the 256 MiB Infinity Cache
+// serves on re-read when the batch is processed column-tile by column-tile.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_subset_exact(const f32x4 *__restrict__ U,
+                                                         int64_t ldu4,
+                                                         const int32_t *__restrict__ sub_off,
+                                                         const int32_t *__restrict__ sub_rows,
+                                                         const float *__restrict__ sub_w,
+                                                         const float *__restrict__ sub_total,
+                                                         int S, int64_t P4,
+                                                         f32x4 *__restrict__ out,
+                                                         int64_t ldo4) {
+    // subset-fastest block order: the S blocks of one column tile run together
+    const int s = blockIdx.x % S;
+    const int64_t tile = blockIdx.x / S;
+    const int64_t i = tile * kBlock + threadIdx.x;
+    if (i >= P4) return;
+    const int beg = sub_off[s], end = sub_off[s + 1];
+    const float b = sub_total[s];
+    FastDiv d;
+    d.b = b;
+    d.y = (float)(1.0 / (double)b);
+    d.fast = (b >= 1.0f && b <= 2147483648.0f) ? 1 : 0;
+    f32x4 acc = term4(load4<NT>(U + (int64_t)sub_rows[beg] * ldu4 + i), sub_w[beg], d);
+    for (int j = beg + 1; j < end; ++j)
+        acc = add4(acc, term4(load4<NT>(U + (int64_t)sub_rows[j] * ldu4 + i), sub_w[j], d));
+    out[(int64_t)s * ldo4 + i] = acc;
+}
+
+}  // namespace
+}  // namespace dls
+
+using namespace dls;
+
+extern "C" int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows,
+                              const float *weight, int32_t K, float total, int64_t P,
+                              int32_t mode, float *out, dls_stream_t stream) {
+    DLS_REQUIRE(U && rows && weight && out, DLS_EINVAL, "dls_fedavg_f32: null pointer");
+    DLS_REQUIRE(K > 0 && P > 0, DLS_EINVAL, "dls_fedavg_f32: K=%d P=%lld", K, (long long)P);
+    DLS_REQUIRE(P % 4 == 0 && ldu % 4 == 0 && ldu >= P, DLS_ELAYOUT,
+                "dls_fedavg_f32: P=%lld and ldu=%lld must be multiples of 4, ldu >= P",
+                (long long)P, (long long)ldu);
+    DLS_REQUIRE(aligned16(U) && aligned16(out), DLS_ELAYOUT, "dls_fedavg_f32: 16-byte alignment");
+    const int64_t P4 = P / 4;
+    const dim3 grid((unsigned)((P4 + kBlock - 1) / kBlock));
+    hipStream_t st = as_stream(stream);
+    if (mode == DLS_FEDAVG_EXACT) {
+        const FastDiv d = make_fastdiv(total);
+        hipLaunchKernelGGL((k_fedavg_exact<8, true>), grid, dim3(kBlock), 0, st,
+                           reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, d,
+                           P4, reinterpret_cast<f32x4 *>(out));
+    } else if (mode == DLS_FEDAVG_FMA) {
+        hipLaunchKernelGGL((k_fedavg_fma<8, true>), grid, dim3(kBlock), 0, st,
+                           reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, total,
+                           P4, reinterpret_cast<f32x4 *>(out));
+    } else {
+        set_error("dls_fedavg_f32: unknown mode %d", mode);
+        return DLS_EINVAL;
+    }
+    return check_launch("dls_fedavg_f32");
+}
+
+extern "C" int dls_subset_fedavg_f32(const float *U, int64_t ldu, const int32_t *sub_off,
+                                     const int32_t *sub_rows, const float *sub_weight,
+                                     const float *sub_total, int32_t S, int64_t P, float *out,
+                                     int64_t ldo, dls_stream_t stream) {
+    DLS_REQUIRE(U && sub_off && sub_rows && sub_weight && sub_total && out, DLS_EINVAL,
+                "dls_subset_fedavg_f32: null pointer");
+    DLS_REQUIRE(S > 0 && P > 0, DLS_EINVAL, "dls_subset_fedavg_f32: S=%d P=%lld", S,
+                (long long)P);
+    DLS_REQUIRE(P % 4 == 0 && ldu % 4 == 0 && ldo % 4 == 0 && ldu >= P && ldo >= P, DLS_ELAYOUT,
+                "dls_subset_fedavg_f32: P, ldu, ldo must be multiples of 4");
+    DLS_REQUIRE(aligned16(U) && aligned16(out), DLS_ELAYOUT,
+                "dls_subset_fedavg_f32: 16-byte alignment");
+    const int64_t P4 = P / 4;
+    const int64_t tiles = (P4 + kBlock - 1) / kBlock;
+    DLS_REQUIRE(tiles * S < (int64_t)1 << 31, DLS_EINVAL, "dls_subset_fedavg_f32: grid too large");
+    hipLaunchKernelGGL((k_subset_exact<false>), dim3((unsigned)(tiles * S)), dim3(kBlock), 0,
+                       as_stream(stream), reinterpret_cast<const f32x4 *>(U), ldu / 4, sub_off,
+                       sub_rows, sub_weight, sub_total, (int)S, P4, reinterpret_cast<f32x4 *>(out),
+                       ldo / 4);
+    return check_launch("dls_subset_fedavg_f32");
+}

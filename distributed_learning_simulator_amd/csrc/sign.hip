@@ -1,0 +1,382 @@
+// signSGD: 2-bit sign planes, majority vote and worker step, for gfx950.
+//
+// Wire format (include/dls_hip.h): per group of 64 parameters two uint64
+// words [pos, neg], bit j = parameter 64g + j; NaN sets both bits.  A client's
+// fp32 sign vector (4 B/param, workers/sign_sgd_worker.py:44) becomes 2 bits/param.
+//
+// Vote (servers/sign_sgd_server.py:12-21): counts = #pos - #neg per parameter,
+// accumulated with bit-sliced ("vertical") counters: one 64-bit word per
+// counter bit holds that bit of 64 parameters' counts, so one client costs
+// 2 x B bitwise ops per plane word (B = ceil(log2(K+1))) and no per-parameter
+// unpacking; the counters are unpacked once at the end.  Exact in any order.
+#include "dls_common.h"
+
+namespace dls {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint64_t spread16(uint64_t x) {
+    // bit k of a 16-bit value -> bit 4k
+    x &= 0xFFFFull;
+    x = (x | (x << 24)) & 0x000000FF000000FFull;
+    x = (x | (x << 12)) & 0x000F000F000F000Full;
+    x = (x | (x << 6)) & 0x0303030303030303ull;
+    x = (x | (x << 3)) & 0x1111111111111111ull;
+    return x;
+}
+
+// One wavefront packs one 256-parameter tile: lane l loads parameters 4l..4l+3
+// (16 B), one 64-lane ballot per component gives bit l = parameter 4l + c, and
+// a scalar 4-way bit interleave turns the four ballots into the natural order.
+__device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile,
+                                          int32_t *nonternary) {
+    const int lane = __lane_id();
+    uint64_t pos[4], neg[4];
+    int bad = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float x = v[c];
+        const bool nan = x != x;
+        pos[c] = __ballot(x > 0.f || nan);
+        neg[c] = __ballot(x < 0.f || nan);
+        bad |= !(x == 0.f || x == 1.f || x == -1.f || nan);
+    }
+    if (nonternary) {
+        const uint64_t b = __ballot(bad);
+        if (b && lane == 0) atomicAdd(nonternary, (int)__popcll(b));
+    }
+    // word m: bit j <- ballot_{j&3} bit (16m + (j>>2)); wave-uniform (scalar) math
+    uint64_t words[8];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        words[2 * m] = spread16(pos[0] >> (16 * m)) | (spread16(pos[1] >> (16 * m)) << 1) |
+                       (spread16(pos[2] >> (16 * m)) << 2) | (spread16(pos[3] >> (16 * m)) << 3);
+        words[2 * m + 1] = spread16(neg[0] >> (16 * m)) | (spread16(neg[1] >> (16 * m)) << 1) |
+                           (spread16(neg[2] >> (16 * m)) << 2) |
+                           (spread16(neg[3] >> (16 * m)) << 3);
+    }
+    uint64_t mine = words[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) mine = (lane == q) ? words[q] : mine;
+    if (lane < 8) dst_tile[lane] = mine;
+}
+
+// grid: x = tile blocks (4 tiles per block), y = client.
+__global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ X, int64_t ldx,
+                                                      int64_t P, uint64_t *__restrict__ planes,
+                                                      int64_t ldp, int64_t ntiles,
+                                                      int32_t *nonternary) {
+    const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;  // wave-uniform
+    const int64_t k = blockIdx.y;
+    const int lane = __lane_id();
+    const int64_t e = tile * 256 + 4 * lane;
+    const float *row = X + k * ldx;
+    f32x4 v;
+    if (e + 4 <= P) {
+        v = *reinterpret_cast<const f32x4 *>(row + e);
+    } else {
+        v = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < 4; ++c)
+            if (e + c < P) v[c] = row[e + c];
+    }
+    pack_tile(v, planes + k * ldp + tile * 8, nonternary);
+}
+
+// ---------------------------------------------------------------- vote
+// Bit-sliced increment: c += x (x one bit per parameter).
+template <int B>
+__device__ __forceinline__ void vinc(uint64_t (&c)[B], uint64_t x) {
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t t = c[b] & x;
+        c[b] ^= x;
+        x = t;
+    }
+}
+
+template <int B>
+__device__ __forceinline__ int unpack_count(const uint64_t (&c)[B], int j) {
+    int v = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) v |= (int)((c[b] >> j) & 1u) << b;
+    return v;
+}
+
+// One lane owns one group of 64 parameters (one 16-byte [pos, neg] load per
+// client).  Outputs: counts (int32, optional) and/or fp32 signs.
+template <int B, int UNROLL>
+__global__ __launch_bounds__(kBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
+                                                      int64_t ldp, const int32_t *__restrict__ rows,
+                                                      int K, int64_t P, int64_t ngroups,
+                                                      int32_t *__restrict__ counts,
+                                                      float *__restrict__ sign_out) {
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= ngroups) return;
+    uint64_t cp[B], cn[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) cp[b] = cn[b] = 0;
+    uint64_t nan = 0;
+    const u64x2 *base = reinterpret_cast<const u64x2 *>(planes) + g;
+    const int64_t ldp2 = ldp / 2;
+    int j = 0;
+    for (; j + UNROLL <= K; j += UNROLL) {
+        u64x2 w[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const int64_t r = rows ? rows[j + u] : (j + u);
+            w[u] = __builtin_nontemporal_load(base + r * ldp2);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            nan |= w[u][0] & w[u][1];
+            vinc<B>(cp, w[u][0]);
+            vinc<B>(cn, w[u][1]);
+        }
+    }
+    for (; j < K; ++j) {
+        const int64_t r = rows ? rows[j] : j;
+        const u64x2 w = __builtin_nontemporal_load(base + r * ldp2);
+        nan |= w[0] & w[1];
+        vinc<B>(cp, w[0]);
+        vinc<B>(cn, w[1]);
+    }
+    const int64_t e0 = g * 64;
+    const bool full = e0 + 64 <= P;
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+        int32_t c4[4];
+        f32x4 s4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int jbit = 4 * q + t;
+            int c = unpack_count<B>(cp, jbit) - unpack_count<B>(cn, jbit);
+            const bool poisoned = (nan >> jbit) & 1u;
+            if (poisoned) c += DLS_SIGN_NAN_MARK;
+            c4[t] = c;
+            s4[t] = poisoned ? 0.f : (c > 0 ? 1.f : (c < 0 ? -1.f : 0.f));
+        }
+        const int64_t e = e0 + 4 * q;
+        if (full) {
+            if (counts)
+                *reinterpret_cast<int4 *>(counts + e) = make_int4(c4[0], c4[1], c4[2], c4[3]);
+            if (sign_out) *reinterpret_cast<f32x4 *>(sign_out + e) = s4;
+        } else {
+            for (int t = 0; t < 4; ++t) {
+                if (e + t < P) {
+                    if (counts) counts[e + t] = c4[t];
+                    if (sign_out) sign_out[e + t] = s4[t];
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ float vote_of(int32_t c) {
+    if (c >= DLS_SIGN_NAN_MARK / 2) return 0.f;
+    return c > 0 ? 1.f : (c < 0 ? -1.f : 0.f);
+}
+
+// counts -> fp32 sign + optional packed vote (one wave per 256-param tile).
+__global__ __launch_bounds__(kBlock) void k_sign_from_counts(const int32_t *__restrict__ counts,
+                                                             int64_t P, int64_t ntiles,
+                                                             float *__restrict__ sign_out,
+                                                             uint64_t *__restrict__ vote_planes) {
+    const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    const int lane = __lane_id();
+    const int64_t e = tile * 256 + 4 * lane;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e + 4 <= P) {
+        const int4 c = *reinterpret_cast<const int4 *>(counts + e);
+        v = f32x4{vote_of(c.x), vote_of(c.y), vote_of(c.z), vote_of(c.w)};
+        if (sign_out) *reinterpret_cast<f32x4 *>(sign_out + e) = v;
+    } else {
+        for (int t = 0; t < 4; ++t)
+            if (e + t < P) {
+                v[t] = vote_of(counts[e + t]);
+                if (sign_out) sign_out[e + t] = v[t];
+            }
+    }
+    if (vote_planes) pack_tile(v, vote_planes + tile * 8, nullptr);
+}
+
+// --------------------------------------------------------------- worker
+// workers/sign_sgd_worker.py:32-44 fused: momentum/dampening/nesterov, sign,
+// pack.  buf.mul_(m).add_(g, alpha=a) == fma(g, a, buf*m); g.add(buf, alpha=m)
+// == fma(buf, m, g) (torch CPU semantics, pinned by the golden vectors).
+__global__ __launch_bounds__(kBlock) void k_sign_sgd_direction(
+    const float *__restrict__ grad, float *__restrict__ buf, int64_t P, int64_t ntiles,
+    float momentum, float a, int nesterov, int first, uint64_t *__restrict__ planes,
+    float *__restrict__ sign_out) {
+    const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    const int lane = __lane_id();
+    const int64_t e = tile * 256 + 4 * lane;
+    f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f}, b = g;
+    const bool full = e + 4 <= P;
+    if (full) {
+        g = *reinterpret_cast<const f32x4 *>(grad + e);
+        if (momentum != 0.f && !first) b = *reinterpret_cast<const f32x4 *>(buf + e);
+    } else {
+        for (int t = 0; t < 4; ++t)
+            if (e + t < P) {
+                g[t] = grad[e + t];
+                if (momentum != 0.f && !first) b[t] = buf[e + t];
+            }
+    }
+    f32x4 d = g;
+    if (momentum != 0.f) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            b[t] = first ? g[t] : __builtin_fmaf(g[t], a, b[t] * momentum);
+            d[t] = nesterov ? __builtin_fmaf(b[t], momentum, g[t]) : b[t];
+        }
+        if (full) {
+            *reinterpret_cast<f32x4 *>(buf + e) = b;
+        } else {
+            for (int t = 0; t < 4; ++t)
+                if (e + t < P) buf[e + t] = b[t];
+        }
+    }
+    f32x4 s;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s[t] = d[t] > 0.f ? 1.f : (d[t] < 0.f ? -1.f : 0.f);  // nan -> 0
+    if (sign_out) {
+        if (full) {
+            *reinterpret_cast<f32x4 *>(sign_out + e) = s;
+        } else {
+            for (int t = 0; t < 4; ++t)
+                if (e + t < P) sign_out[e + t] = s[t];
+        }
+    }
+    if (!full) {
+        for (int t = 0; t < 4; ++t)
+            if (e + t >= P) s[t] = 0.f;
+    }
+    pack_tile(s, planes + tile * 8, nullptr);
+}
+
+// workers/sign_sgd_worker.py:48-57: d = vote (+ fma(p, wd, vote)); p = fma(d, -lr, p).
+__global__ __launch_bounds__(kBlock) void k_sign_sgd_apply(float *__restrict__ param,
+                                                           const uint64_t *__restrict__ vote,
+                                                           int64_t P, float neg_lr, float wd) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // 4 params each
+    const int64_t e = i * 4;
+    if (e >= P) return;
+    const int64_t g = e >> 6;
+    const int sh = (int)(e & 63);
+    const uint64_t pw = vote[2 * g], nw = vote[2 * g + 1];
+    for (int t = 0; t < 4 && e + t < P; ++t) {
+        const int pb = (int)((pw >> (sh + t)) & 1u), nb = (int)((nw >> (sh + t)) & 1u);
+        float d = (pb && !nb) ? 1.f : ((nb && !pb) ? -1.f : 0.f);
+        float p = param[e + t];
+        if (wd != 0.f) d = __builtin_fmaf(p, wd, d);
+        param[e + t] = __builtin_fmaf(d, neg_lr, p);
+    }
+}
+
+template <int B>
+int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K, int64_t P,
+                int32_t *counts, float *sign_out, hipStream_t st) {
+    const int64_t ngroups = (P + 63) / 64;
+    const dim3 grid((unsigned)((ngroups + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL((k_sign_vote<B, 8>), grid, dim3(kBlock), 0, st, planes, ldp, rows, K, P,
+                       ngroups, counts, sign_out);
+    return check_launch("dls_sign_vote");
+}
+
+int vote_dispatch(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K, int64_t P,
+                  int32_t *counts, float *sign_out, hipStream_t st) {
+    // counter width B: K <= 2^B - 1 (fewer bits = fewer ops and registers)
+    if (K < (1 << 4)) return launch_vote<4>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (K < (1 << 8)) return launch_vote<8>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (K < (1 << 10)) return launch_vote<10>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (K < (1 << 12)) return launch_vote<12>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (K < (1 << 16)) return launch_vote<16>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (K < (1 << 20)) return launch_vote<20>(planes, ldp, rows, K, P, counts, sign_out, st);
+    set_error("dls_sign_vote: K=%d exceeds 2^20-1 clients", K);
+    return DLS_EINVAL;
+}
+
+}  // namespace
+}  // namespace dls
+
+using namespace dls;
+
+extern "C" int dls_sign_pack_f32(const float *X, int64_t ldx, int32_t K, int64_t P,
+                                 uint64_t *planes, int64_t ldp, int32_t *nonternary,
+                                 dls_stream_t stream) {
+    DLS_REQUIRE(X && planes, DLS_EINVAL, "dls_sign_pack_f32: null pointer");
+    DLS_REQUIRE(K > 0 && P > 0 && K < 65536, DLS_EINVAL, "dls_sign_pack_f32: K=%d P=%lld", K,
+                (long long)P);
+    DLS_REQUIRE(ldx >= P && ldp >= DLS_SIGN_WORDS(P) && ldx % 4 == 0 && aligned16(X), DLS_ELAYOUT,
+                "dls_sign_pack_f32: ldx=%lld (multiple of 4, >= P) ldp=%lld (>= %lld)",
+                (long long)ldx, (long long)ldp, (long long)DLS_SIGN_WORDS(P));
+    const int64_t ntiles = (P + 255) / 256;
+    const dim3 grid((unsigned)((ntiles + 3) / 4), (unsigned)K);
+    hipLaunchKernelGGL(k_sign_pack, grid, dim3(kBlock), 0, as_stream(stream), X, ldx, P, planes,
+                       ldp, ntiles, nonternary);
+    return check_launch("dls_sign_pack_f32");
+}
+
+extern "C" int dls_sign_vote_count(const uint64_t *planes, int64_t ldp, const int32_t *rows,
+                                   int32_t K, int64_t P, int32_t *counts, dls_stream_t stream) {
+    DLS_REQUIRE(planes && counts, DLS_EINVAL, "dls_sign_vote_count: null pointer");
+    DLS_REQUIRE(K > 0 && P > 0, DLS_EINVAL, "dls_sign_vote_count: K=%d P=%lld", K, (long long)P);
+    DLS_REQUIRE(ldp >= DLS_SIGN_WORDS(P) && ldp % 2 == 0 && aligned16(planes) && P % 4 == 0 &&
+                    aligned16(counts),
+                DLS_ELAYOUT, "dls_sign_vote_count: layout (ldp=%lld, P=%lld)", (long long)ldp,
+                (long long)P);
+    return vote_dispatch(planes, ldp, rows, K, P, counts, nullptr, as_stream(stream));
+}
+
+extern "C" int dls_sign_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K,
+                             int64_t P, int32_t *counts, float *sign_out, dls_stream_t stream) {
+    DLS_REQUIRE(planes && sign_out, DLS_EINVAL, "dls_sign_vote: null pointer");
+    DLS_REQUIRE(K > 0 && P > 0, DLS_EINVAL, "dls_sign_vote: K=%d P=%lld", K, (long long)P);
+    DLS_REQUIRE(ldp >= DLS_SIGN_WORDS(P) && ldp % 2 == 0 && aligned16(planes) && P % 4 == 0 &&
+                    aligned16(sign_out) && (!counts || aligned16(counts)),
+                DLS_ELAYOUT, "dls_sign_vote: layout (ldp=%lld, P=%lld)", (long long)ldp,
+                (long long)P);
+    return vote_dispatch(planes, ldp, rows, K, P, counts, sign_out, as_stream(stream));
+}
+
+extern "C" int dls_sign_from_counts(const int32_t *counts, int64_t P, float *sign_out,
+                                    uint64_t *vote_planes, dls_stream_t stream) {
+    DLS_REQUIRE(counts && (sign_out || vote_planes), DLS_EINVAL,
+                "dls_sign_from_counts: null pointer");
+    DLS_REQUIRE(P > 0 && P % 4 == 0 && aligned16(counts) && (!sign_out || aligned16(sign_out)),
+                DLS_ELAYOUT, "dls_sign_from_counts: P=%lld must be a multiple of 4", (long long)P);
+    const int64_t ntiles = (P + 255) / 256;
+    hipLaunchKernelGGL(k_sign_from_counts, dim3((unsigned)((ntiles + 3) / 4)), dim3(kBlock), 0,
+                       as_stream(stream), counts, P, ntiles, sign_out, vote_planes);
+    return check_launch("dls_sign_from_counts");
+}
+
+extern "C" int dls_sign_sgd_direction(const float *grad, float *buf, int64_t P, float momentum,
+                                      float one_minus_dampening, int32_t nesterov, int32_t first,
+                                      uint64_t *planes, float *sign_out, dls_stream_t stream) {
+    DLS_REQUIRE(grad && planes && (momentum == 0.f || buf), DLS_EINVAL,
+                "dls_sign_sgd_direction: null pointer");
+    DLS_REQUIRE(P > 0, DLS_EINVAL, "dls_sign_sgd_direction: P=%lld", (long long)P);
+    DLS_REQUIRE(aligned16(grad) && (!buf || aligned16(buf)) && (!sign_out || aligned16(sign_out)),
+                DLS_ELAYOUT, "dls_sign_sgd_direction: 16-byte alignment");
+    const int64_t ntiles = (P + 255) / 256;
+    hipLaunchKernelGGL(k_sign_sgd_direction, dim3((unsigned)((ntiles + 3) / 4)), dim3(kBlock), 0,
+                       as_stream(stream), grad, buf, P, ntiles, momentum, one_minus_dampening,
+                       (int)nesterov, (int)first, planes, sign_out);
+    return check_launch("dls_sign_sgd_direction");
+}
+
+extern "C" int dls_sign_sgd_apply(float *param, const uint64_t *vote_planes, int64_t P,
+                                  float neg_lr, float weight_decay, dls_stream_t stream) {
+    DLS_REQUIRE(param && vote_planes, DLS_EINVAL, "dls_sign_sgd_apply: null pointer");
+    DLS_REQUIRE(P > 0, DLS_EINVAL, "dls_sign_sgd_apply: P=%lld", (long long)P);
+    const int64_t threads = (P + 3) / 4;
+    hipLaunchKernelGGL(k_sign_sgd_apply, dim3((unsigned)((threads + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, as_stream(stream), param, vote_planes, P, neg_lr,
+                       weight_decay);
+    return check_launch("dls_sign_sgd_apply");
+}

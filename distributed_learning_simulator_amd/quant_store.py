@@ -1,0 +1,181 @@
+"""Device store of quantized client payloads for the fed_quant server.
+
+Reference payload (servers/fed_quant_server.py:25-33, produced by the QAT
+worker, workers/fed_quant_worker.py:40): ``{name: (int weight [C, ...],
+scale [C], zero_point [C]) | fp32 tensor}``.  The reference materialises every
+client's fp32 dequantized tensors; here the int payloads stay int in HBM and
+one fused kernel (``dls_dequant_fedavg``) dequantizes and averages them.
+
+HBM layout per client row:
+  Q  uint8 [capacity, ldq]   int tensors' raw bytes (int8 or uint8), 64-B aligned
+  F  fp32  [capacity, ldf]   fp32 tensors (biases ...), 64-element aligned
+  sz fp32  [capacity, C+1, 2] per output channel (fl32(scale), zero_point)
+and a tile table (``dls_qtile``) built once per layout: tiles of <= 4096
+elements inside one tensor, which also carry the channel bookkeeping.
+"""
+import numpy as np
+import torch
+
+from . import _native
+from .layout import ALIGN, ParameterLayout, _round_up
+
+TILE = 4096
+
+QTILE_DTYPE = np.dtype([("dst", "<i8"), ("src", "<i8"), ("len", "<i4"), ("kind", "<i4"),
+                        ("chan0", "<i4"), ("row_len", "<i4"), ("row_pos", "<i4"),
+                        ("chan_end", "<i4")])
+assert QTILE_DTYPE.itemsize == 40
+
+
+def _int_repr(w):
+    if w.is_quantized:
+        w = w.int_repr()
+    if w.dtype not in (torch.int8, torch.uint8):
+        raise TypeError(f"quantized weight must be int8/uint8, got {w.dtype}")
+    return w
+
+
+def is_quantized_entry(v):
+    return isinstance(v, tuple) and len(v) == 3
+
+
+class QuantLayout:
+    """Per-tensor kinds and offsets for one payload structure."""
+
+    def __init__(self, payload):
+        items = []
+        self.kinds, self.src, self.chan_base, self.channels, self.row_len = [], [], [], [], []
+        q_off = f_off = c_off = 0
+        for name, v in payload.items():
+            if is_quantized_entry(v):
+                w = _int_repr(v[0])
+                shape = tuple(w.shape)
+                kind = 1 if w.dtype == torch.int8 else 2
+                C = shape[0] if shape else 1
+                n = int(np.prod(shape)) if shape else 1
+                self.kinds.append(kind)
+                self.src.append(q_off)
+                self.chan_base.append(c_off)
+                self.channels.append(C)
+                self.row_len.append(max(1, n // C))
+                q_off += _round_up(max(n, 1), ALIGN)
+                c_off += C
+            else:
+                shape = tuple(v.shape)
+                n = int(np.prod(shape)) if shape else 1
+                self.kinds.append(0)
+                self.src.append(f_off)
+                self.chan_base.append(0)
+                self.channels.append(0)
+                self.row_len.append(1)
+                f_off += _round_up(max(n, 1), ALIGN)
+            items.append((name, shape))
+        self.layout = ParameterLayout(items)
+        self.ldq = max(q_off, ALIGN)
+        self.ldf = max(f_off, ALIGN)
+        self.C = c_off
+        self.names = self.layout.names
+
+    def matches(self, payload):
+        if list(payload.keys()) != self.names:
+            return False
+        for v, kind, shape in zip(payload.values(), self.kinds, self.layout.shapes):
+            if (kind > 0) != is_quantized_entry(v):
+                return False
+            t = v[0] if kind else v
+            if tuple(t.shape) != shape:
+                return False
+        return True
+
+    def tiles(self):
+        rows = []
+        for i, kind in enumerate(self.kinds):
+            n = self.layout.numels[i]
+            for e in range(0, n, TILE):
+                ln = min(TILE, n - e)
+                rl = self.row_len[i]
+                rows.append((self.layout.offsets[i] + e, self.src[i] + e, ln, kind,
+                             self.chan_base[i] + e // rl if kind else 0, rl,
+                             e % rl if kind else 0,
+                             self.chan_base[i] + self.channels[i] if kind else 0))
+        return np.array(rows, dtype=QTILE_DTYPE)
+
+
+class QuantizedClientStore:
+    def __init__(self, payload, device, capacity=1):
+        self.qlayout = QuantLayout(payload)
+        self.layout = self.qlayout.layout
+        self.device = torch.device(device)
+        cap = max(1, capacity)
+        ql = self.qlayout
+        self.Q = torch.zeros((cap, ql.ldq), dtype=torch.uint8, device=self.device)
+        self.F = torch.zeros((cap, ql.ldf), dtype=torch.float32, device=self.device)
+        self.sz = torch.zeros((cap, ql.C + 1, 2), dtype=torch.float32, device=self.device)
+        t = ql.tiles()
+        self.ntiles = len(t)
+        self.tiles = torch.from_numpy(t.view(np.uint8).copy()).to(self.device)
+        self._free = list(range(cap))[::-1]
+
+    @property
+    def capacity(self):
+        return self.Q.shape[0]
+
+    def acquire(self):
+        if not self._free:
+            old = (self.Q, self.F, self.sz)
+            cap = 2 * old[0].shape[0]
+            self.Q = torch.zeros((cap,) + tuple(old[0].shape[1:]), dtype=old[0].dtype,
+                                 device=self.device)
+            self.F = torch.zeros((cap,) + tuple(old[1].shape[1:]), dtype=old[1].dtype,
+                                 device=self.device)
+            self.sz = torch.zeros((cap,) + tuple(old[2].shape[1:]), dtype=old[2].dtype,
+                                  device=self.device)
+            n = old[0].shape[0]
+            self.Q[:n].copy_(old[0])
+            self.F[:n].copy_(old[1])
+            self.sz[:n].copy_(old[2])
+            self._free = list(range(n, cap))[::-1]
+        return self._free.pop()
+
+    def release(self, row):
+        self._free.append(row)
+
+    def write(self, row, payload):
+        ql = self.qlayout
+        for i, (name, v) in enumerate(payload.items()):
+            n = self.layout.numels[i]
+            if ql.kinds[i]:
+                w, scale, zp = v
+                w = _int_repr(w)
+                self.Q[row, ql.src[i]:ql.src[i] + n].copy_(
+                    w.reshape(-1).view(torch.uint8), non_blocking=True)
+                cb, C = ql.chan_base[i], ql.channels[i]
+                # torch casts the 0-dim float64 scale / int64 zero point to fp32
+                # before the fp32 ops (servers/fed_quant_server.py:31)
+                s32 = torch.as_tensor(scale).reshape(-1).to(torch.float32)
+                z32 = torch.as_tensor(zp).reshape(-1).to(torch.float32)
+                self.sz[row, cb:cb + C, 0].copy_(s32, non_blocking=True)
+                self.sz[row, cb:cb + C, 1].copy_(z32, non_blocking=True)
+            else:
+                self.F[row, ql.src[i]:ql.src[i] + n].copy_(v.reshape(-1).float(),
+                                                           non_blocking=True)
+
+    def fedavg(self, rows, ns, out=None):
+        if out is None:
+            out = torch.empty(self.layout.P, dtype=torch.float32, device=self.device)
+        total = sum(int(n) for n in ns)
+        rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
+        w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
+        _native.dequant_fedavg(self.tiles, self.ntiles, self.Q, self.F, self.sz, rows_t, w_t,
+                               float(total), out)
+        return out
+
+    def dequantize(self, row):
+        """One client's fp32 dict (the reference's _process_client_parameter output)."""
+        return self.layout.views(self.fedavg([row], [1]))
+
+    def accepts(self, payload):
+        return self.qlayout.matches(payload)
+
+    def views(self, row):
+        return self.dequantize(row)

@@ -1,0 +1,91 @@
+"""FedAvg server (reference: servers/fed_server.py:11-91).
+
+Same hooks, same round protocol, same return objects; ``get_subset_model`` is
+one ``dls_fedavg_f32`` launch over the clients' HBM rows instead of a Python
+loop of K x (#tensors) torch ops, bit-exact with the reference's op order.
+"""
+import copy
+import logging
+
+from .. import _native
+from ..aggregation import ClientParameters, ClientUpdateStore
+from ..layout import ParameterLayout
+from ..model_util import ModelUtil
+from ..task_queue import RepeatedResult
+from .server import Server
+
+log = logging.getLogger("distributed_learning_simulator_amd")
+
+_MODES = {"exact": _native.FEDAVG_EXACT, "fma": _native.FEDAVG_FMA}
+
+
+class FedServer(Server):
+    def __init__(self, aggregation_mode="exact", **kwargs):
+        super().__init__(**kwargs)
+        _native.require_gpu()
+        self.round = 0
+        self.aggregation_mode = aggregation_mode
+        self.parameters: ClientParameters = ClientParameters(self._make_store)
+        self.__prev_model = copy.deepcopy(
+            ModelUtil(self.tester.model).get_parameter_dict()) if self.tester is not None else {}
+        self.worker_data_queue.put_result(
+            RepeatedResult(data=self.prev_model, num=self.worker_number))
+
+    def _make_store(self, parameter_dict):
+        return ClientUpdateStore(ParameterLayout.from_dict(parameter_dict), self.device,
+                                 capacity=self.worker_number)
+
+    def get_metric(self, model, metric_type="acc"):
+        """servers/fed_server.py:26-32 — load, run the tester, top-1 accuracy or loss."""
+        if self.tester is None:
+            return None
+        ModelUtil(self.tester.model).load_parameter_dict(model)
+        self.tester.inference()
+        if metric_type == "acc":
+            return self.tester.accuracy_metric.get_accuracy(1)
+        return self.tester.loss_metric.get_loss(1).data.item()
+
+    @property
+    def prev_model(self):
+        return self.__prev_model
+
+    def _set_prev_model(self, model):
+        self.__prev_model = model
+
+    def _process_client_parameter(self, client_parameter: dict):
+        return client_parameter
+
+    def _process_aggregated_parameter(self, aggregated_parameter: dict):
+        return aggregated_parameter
+
+    def get_subset_model(self, client_subset):
+        """servers/fed_server.py:44-66 (empty subset -> previous model)."""
+        if not client_subset:
+            return self.__prev_model
+        ids = list(client_subset)
+        store = self.parameters.store
+        flat = self._aggregate(store, [self.parameters.row_of(i) for i in ids],
+                               [self.parameters.n_of(i) for i in ids])
+        return store.layout.views(flat)
+
+    def _aggregate(self, store, rows, ns):
+        return store.fedavg(rows, ns, mode=_MODES[self.aggregation_mode])
+
+    def _process_worker_data(self, data, __):
+        worker_id, training_dataset_size, parameter_dict = data
+        self.parameters[worker_id] = (
+            training_dataset_size,
+            self._process_client_parameter(parameter_dict),
+        )
+        if len(self.parameters) != self.worker_number:
+            log.debug("%s %s,skip", len(self.parameters), self.worker_number)
+            return None
+        self.round += 1
+        log.info("begin aggregating")
+        avg_parameter = self.get_subset_model(self.parameters.keys())
+        data = self._process_aggregated_parameter(avg_parameter)
+        self.__prev_model = copy.deepcopy(data)
+        acc = self.get_metric(self.prev_model)
+        log.info("end aggregating, test accuracy is %s", acc)
+        self.parameters.clear()
+        return RepeatedResult(data=data, num=self.worker_number)

@@ -1,0 +1,180 @@
+/*
+ * dls_hip.h — C-ABI of libdls_hip.so, the MI355X (gfx950) implementation of the
+ * server-side aggregation hot path of chen-zichen/distributed_learning_simulator.
+ *
+ * Every entry point replaces one reference hook (file:line in the reference
+ * repository) and is called from the Python host layer
+ * (distributed_learning_simulator_amd/_native.py, via ctypes).
+ *
+ * Contract:
+ *   - plain pointers and sizes; every array argument is DEVICE memory owned by
+ *     the caller (allocated by torch); nothing is retained after return;
+ *   - `stream` is a hipStream_t passed as void*; every launch is asynchronous on
+ *     it; no entry point synchronises, allocates or frees (graph-capturable);
+ *   - return 0 on success, a negative DLS_E* code for a bad argument, or a
+ *     positive hipError_t; dls_last_error() then describes it (thread-local);
+ *   - all entry points are re-entrant; nothing throws across the ABI.
+ *
+ * Flattened parameter layout ("flat rows"): a client's parameter dict is one row
+ * of a client-major matrix, tensors concatenated in dict (named_parameters)
+ * order, each tensor starting at a multiple of 64 elements; `ld*` is the row
+ * stride in elements.
+ */
+#ifndef DLS_HIP_H
+#define DLS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLS_ABI_VERSION 1
+
+#define DLS_OK 0
+#define DLS_EINVAL (-1)     /* bad size / null pointer / unsupported mode */
+#define DLS_ELAYOUT (-2)    /* misaligned pointer or leading dimension */
+
+/* FedAvg modes */
+#define DLS_FEDAVG_EXACT 0  /* reference op order: acc (+)= fl(fl(x*n_i)/N) in client order; bit-exact */
+#define DLS_FEDAVG_FMA 1    /* acc = fma(x, w_i, acc) with w_i = fl(n_i/N); normwise ~1e-7 */
+
+/* Sign planes: parameters are grouped by 64; group g is two uint64 words,
+ * word 2g = "positive" plane, word 2g+1 = "negative" plane, bit j of either
+ * is parameter 64*g + j.  NaN sets both bits; parameters past P are 0.
+ * A client row holds DLS_SIGN_WORDS(P) words (padded to whole 256-param
+ * tiles, 8 words per tile). */
+#define DLS_SIGN_TILE 256
+#define DLS_SIGN_WORDS(P) ((((P) + 255) / 256) * 8)
+/* Vote counts: #pos - #neg, plus DLS_SIGN_NAN_MARK if any counted client sent
+ * NaN for that parameter; a count >= DLS_SIGN_NAN_MARK/2 decodes as "poisoned"
+ * (vote 0), which survives an int32 sum over up to 127 ranks. */
+#define DLS_SIGN_NAN_MARK (1 << 24)
+
+typedef void *dls_stream_t;
+
+const char *dls_last_error(void);
+int dls_abi_version(void);
+int dls_device_count(void);
+
+/* ------------------------------------------------------------------ FedAvg
+ * Replaces FedServer.get_subset_model (servers/fed_server.py:44-66) for a
+ * non-empty subset.
+ *   U      fp32 [*, ldu]    client rows (flat parameter layout)
+ *   rows   int32 [K]        row of U for each client, in the reference's
+ *                           iteration order (dict key order / subset tuple)
+ *   weight fp32 [K]         fl32(n_i): the Python int sample counts as torch
+ *                           converts them (fed_server.py:59)
+ *   total  fl32(sum n_i)    (fed_server.py:51-53,60)
+ *   out    fp32 [P]         out = first term, then += (fed_server.py:62-65)
+ * P, ldu multiples of 4; U and out 16-byte aligned. */
+int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows, const float *weight,
+                   int32_t K, float total, int64_t P, int32_t mode, float *out,
+                   dls_stream_t stream);
+
+/* Batched subset aggregation in reference order: S subsets at once.
+ * Subset s lists sub_rows[sub_off[s] .. sub_off[s+1]) with matching
+ * sub_weight[], divisor sub_total[s]; result row s of out [S, ldo].
+ * Replaces the get_subset_model calls of the Shapley servers
+ * (servers/GTG_shapley_value_server.py:56, multiround_shapley_value_server.py:37). */
+int dls_subset_fedavg_f32(const float *U, int64_t ldu, const int32_t *sub_off,
+                          const int32_t *sub_rows, const float *sub_weight,
+                          const float *sub_total, int32_t S, int64_t P, float *out,
+                          int64_t ldo, dls_stream_t stream);
+
+/* Subset aggregation as a dense fp32 MFMA contraction: out[S, P] = C[S, K] · U[rows, P]
+ * (C row-major [S, K], c_si = n_i / N_S; rows[K] selects the K client rows of U).
+ * fp32 in / fp32 accumulate (v_mfma_f32_32x32x2_f32): an fma chain in client
+ * order, normwise ~1e-7 from the exact weighted mean. */
+int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const float *U, int64_t ldu,
+                        const int32_t *rows, int64_t P, float *out, int64_t ldo,
+                        dls_stream_t stream);
+
+/* -------------------------------------------------------------- sign vote
+ * Producer side of workers/sign_sgd_worker.py:44 (torch.sign) + the 16x smaller
+ * wire format: pack fp32 vectors X [K, ldx] into planes [K, ldp] (ldp >=
+ * DLS_SIGN_WORDS(P)).  Values other than -1, 0, +1, NaN are counted into
+ * *nonternary (device int32, accumulated; caller zeroes it) when it is
+ * non-null, because the vote of such inputs would differ from the reference's
+ * fp32 sum. */
+int dls_sign_pack_f32(const float *X, int64_t ldx, int32_t K, int64_t P, uint64_t *planes,
+                      int64_t ldp, int32_t *nonternary, dls_stream_t stream);
+
+/* SignSGDServer.__worker (servers/sign_sgd_server.py:12-21): counts[p] =
+ * sum over the K client rows of (+1 pos, -1 neg, +NAN_MARK nan).  `rows` may be
+ * NULL (rows 0..K-1).  counts may be all-reduced (int32 sum) across ranks. */
+int dls_sign_vote_count(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K,
+                        int64_t P, int32_t *counts, dls_stream_t stream);
+
+/* counts -> torch.sign(sum) as fp32 {-1, +0, +1} (NaN-poisoned -> 0, as CPU
+ * torch.sign(nan)), and optionally the vote packed in the plane format. */
+int dls_sign_from_counts(const int32_t *counts, int64_t P, float *sign_out,
+                         uint64_t *vote_planes, dls_stream_t stream);
+
+/* Fused single-device vote: planes -> fp32 signs (counts optional, may be NULL). */
+int dls_sign_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K,
+                  int64_t P, int32_t *counts, float *sign_out, dls_stream_t stream);
+
+/* Worker step, workers/sign_sgd_worker.py:32-44 fused: momentum / dampening /
+ * nesterov on grad (buf updated in place; first=1 clones), torch.sign, pack to
+ * planes (ldp words), optional fp32 sign copy.  a = fl32(1 - dampening). */
+int dls_sign_sgd_direction(const float *grad, float *buf, int64_t P, float momentum,
+                           float one_minus_dampening, int32_t nesterov, int32_t first,
+                           uint64_t *planes, float *sign_out, dls_stream_t stream);
+
+/* workers/sign_sgd_worker.py:48-57: p = fma(vote + wd*p, -lr, p) with the vote
+ * read from packed planes (NaN-poisoned or tied -> 0). */
+int dls_sign_sgd_apply(float *param, const uint64_t *vote_planes, int64_t P, float neg_lr,
+                       float weight_decay, dls_stream_t stream);
+
+/* ----------------------------------------------------------------- quant
+ * Tile of the flattened parameter space for the fused dequant-FedAvg kernel.
+ * A tile lies inside one tensor; host code builds the table once per layout. */
+typedef struct dls_qtile {
+    int64_t dst;     /* first output element (flat layout offset, multiple of 16) */
+    int64_t src;     /* first element within a client row of Q (kind 1/2) or F (kind 0) */
+    int32_t len;     /* elements, <= 4096; lanes cover 16-element chunks up to the
+                        next multiple of 64 (the rows are padded to 64) and write
+                        0 past len, so the output's row padding is always zero */
+    int32_t kind;    /* 0 = fp32 tensor, 1 = int8 per-channel, 2 = uint8 per-channel */
+    int32_t chan0;   /* channel (index into the client's scale/zp row) of element 0 */
+    int32_t row_len; /* elements per output channel */
+    int32_t row_pos; /* position of element 0 inside its channel row */
+    int32_t chan_end; /* one past the tensor's last channel (clamps padded tails) */
+} dls_qtile;
+
+/* FedQuantServer._process_client_parameter (servers/fed_quant_server.py:25-33)
+ * fused into FedServer.get_subset_model (servers/fed_server.py:44-66):
+ *   out[e] (+)= fl(fl(fl(fl(q - zp[c]) * scale[c]) * n_i) / N)  (int tensors)
+ *   out[e] (+)= fl(fl(x * n_i) / N)                              (fp32 tensors)
+ * bit-exact in client order.  Q int8/uint8 [*, ldq], F fp32 [*, ldf],
+ * sz fp32 pairs [*, ldc] of (fl32(scale), zero_point) per channel. */
+int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const void *Q, int64_t ldq,
+                       const float *F, int64_t ldf, const float *sz, int64_t ldc,
+                       const int32_t *rows, const float *weight, int32_t K, float total,
+                       float *out, dls_stream_t stream);
+
+/* Per-segment min / max of x over [seg_off[s], seg_off[s+1]) (torch.aminmax);
+ * seg_off is device int64 [nseg+1] with seg_off[nseg] == total.  NaNs are
+ * ignored (fminf/fmaxf). */
+int dls_segment_minmax_f32(const float *x, const int64_t *seg_off, int32_t nseg, float *mins,
+                           float *maxs, int64_t total, dls_stream_t stream);
+
+/* MinMaxObserver-style affine qparams on device (fp32): for each segment
+ * scale = max((max(hi,0) - min(lo,0)) / (qmax - qmin), eps),
+ * zp = clamp(qmin - rne(min(lo,0) / scale), qmin, qmax). */
+int dls_qparams_minmax(const float *mins, const float *maxs, int32_t nseg, int32_t qmin,
+                       int32_t qmax, float *scale, int32_t *zp, dls_stream_t stream);
+
+/* Affine quantize per segment: q = clamp(rne(x * fl(1/scale)) + zp, 0, 255)
+ * (torch quantize_per_tensor); stochastic=1 replaces rne by floor(v + u),
+ * u = counter-based uniform(seed, element).  deq (optional) =
+ * fl(fl(q - zp) * scale). */
+int dls_quantize_u8(const float *x, const int64_t *seg_off, int32_t nseg, const float *scale,
+                    const int32_t *zp, uint8_t *q, float *deq, int32_t stochastic, uint64_t seed,
+                    int64_t total, dls_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLS_HIP_H */

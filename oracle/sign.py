@@ -16,12 +16,11 @@ Reference worker: ``SignSGDWorker.__get_gredient``, workers/sign_sgd_worker.py:1
 multiply-add ``fma(x, fl32(a), self)`` on the CPU (checked against the golden
 vectors).
 
-Wire format of the packed planes (the HIP kernels' layout, restated here so
-tests can check the packing bit-for-bit): parameters are grouped in tiles of
-256; tile ``t`` is 8 uint64 words ``[pos_0, neg_0, pos_1, neg_1, pos_2, neg_2,
-pos_3, neg_3]`` and bit ``l`` of ``pos_c``/``neg_c`` is parameter
-``256*t + 4*l + c`` (one 16-byte float4 per wavefront lane, one 64-lane ballot
-per component).  pos = (x > 0), neg = (x < 0); NaN sets both bits.
+Wire format of the packed planes (the HIP kernels' layout, include/dls_hip.h,
+restated here so tests can check the packing bit-for-bit): parameters are
+grouped by 64; group ``g`` is two uint64 words ``[pos_g, neg_g]`` and bit ``j``
+of either is parameter ``64*g + j``; rows are padded to whole tiles of 256
+parameters.  pos = (x > 0), neg = (x < 0); NaN sets both bits.
 """
 import numpy as np
 
@@ -37,26 +36,33 @@ def pack_planes(x):
     xp = np.zeros(T * TILE, np.float32)
     xp[:P] = x
     nan = np.isnan(xp)
-    pos = (xp > 0) | nan
-    neg = (xp < 0) | nan
-    # param index = 256 t + 4 l + c  ->  array [t, l, c]
-    pos = pos.reshape(T, 64, 4)
-    neg = neg.reshape(T, 64, 4)
+    pos = ((xp > 0) | nan).reshape(-1, 64).astype(np.uint64)
+    neg = ((xp < 0) | nan).reshape(-1, 64).astype(np.uint64)
     weights = (np.uint64(1) << np.arange(64, dtype=np.uint64))
-    out = np.zeros((T, 4, 2), np.uint64)
-    for c in range(4):
-        out[:, c, 0] = (pos[:, :, c].astype(np.uint64) * weights).sum(1, dtype=np.uint64)
-        out[:, c, 1] = (neg[:, :, c].astype(np.uint64) * weights).sum(1, dtype=np.uint64)
+    out = np.zeros((pos.shape[0], 2), np.uint64)
+    out[:, 0] = (pos * weights).sum(1, dtype=np.uint64)
+    out[:, 1] = (neg * weights).sum(1, dtype=np.uint64)
     return out.reshape(-1)
 
 
+def unpack_planes(planes, P):
+    """uint64 planes -> fp32 {-1, 0, +1, nan} [P] (inverse of pack_planes)."""
+    w = np.asarray(planes, np.uint64).reshape(-1, 2)
+    sh = np.arange(64, dtype=np.uint64)
+    pos = ((w[:, 0:1] >> sh) & np.uint64(1)).reshape(-1).astype(bool)
+    neg = ((w[:, 1:2] >> sh) & np.uint64(1)).reshape(-1).astype(bool)
+    out = pos.astype(np.float32) - neg.astype(np.float32)
+    out[pos & neg] = np.nan
+    return out[:P]
+
+
 def vote_counts(S):
-    """int32 counts = #pos - #neg (+ NAN_MARK per client holding a NaN)."""
+    """int32 counts = #pos - #neg (+ NAN_MARK if any client sent a NaN)."""
     S = np.asarray(S, dtype=np.float32)
     nan = np.isnan(S)
     pos = (S > 0).sum(0)
     neg = (S < 0).sum(0)
-    return (pos - neg + NAN_MARK * nan.sum(0)).astype(np.int32)
+    return (pos - neg + NAN_MARK * nan.any(0)).astype(np.int32)
 
 
 def vote_from_counts(c):

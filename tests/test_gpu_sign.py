@@ -1,0 +1,174 @@
+"""GPU parity: sign pack / vote / worker step vs the oracle and golden vectors (bit-exact)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import sign as osign
+from tests import golden as G
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda")
+
+
+def same_bits(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    nan = np.isnan(a)
+    return np.array_equal(nan, np.isnan(b)) and np.array_equal(
+        a.view(np.uint32)[~nan], b.view(np.uint32)[~nan])
+
+
+def pack(S):
+    from distributed_learning_simulator_amd import _native
+    K, P = S.shape
+    Pp = (P + 3) // 4 * 4
+    X = torch.zeros((K, Pp), dtype=torch.float32)
+    X[:, :P] = torch.from_numpy(np.ascontiguousarray(S))
+    X = X.to(dev)
+    planes = torch.full((K, _native.sign_words(P)), 0xAB, dtype=torch.int64, device=dev)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    _native.sign_pack(X, P, planes, bad)
+    return planes, int(bad.item())
+
+
+def test_pack_matches_wire_format():
+    g = np.random.default_rng(0)
+    for P in (1, 63, 64, 255, 256, 1000, 4096 + 68):
+        S = np.sign(g.standard_normal((3, P))).astype(np.float32)
+        S[:, ::13] = 0
+        S[1, P // 2] = np.nan
+        planes, bad = pack(S)
+        assert bad == 0
+        got = planes.cpu().numpy().view(np.uint64)
+        for k in range(3):
+            assert np.array_equal(got[k], osign.pack_planes(S[k])), (P, k)
+
+
+def test_pack_flags_nonternary():
+    S = np.array([[1.0, 0.5, -1.0, 2.0, 0.0, np.inf, -0.0, np.nan]], np.float32)
+    _, bad = pack(S)
+    assert bad == 3  # 0.5, 2.0, inf
+
+
+def test_vote_golden_bit_exact():
+    from distributed_learning_simulator_amd import _native
+    z = G.load("sign_vote.npz")
+    for case in G.meta(z):
+        S, vote = z[f"{case['key']}_signs"], z[f"{case['key']}_vote"]
+        K, P = S.shape
+        planes, _ = pack(S)
+        Pp = (P + 3) // 4 * 4
+        out = torch.empty(Pp, device=dev)
+        counts = torch.empty(Pp, dtype=torch.int32, device=dev)
+        _native.sign_vote(planes, None, K, Pp, out, counts)
+        assert same_bits(out.cpu().numpy()[:P], vote), case["key"]
+        assert np.array_equal(counts.cpu().numpy()[:P], osign.vote_counts(S))
+        # two-stage path (what the multi-GPU server uses): counts -> sign + packed vote
+        c2 = torch.empty(Pp, dtype=torch.int32, device=dev)
+        _native.sign_vote_count(planes, None, K, Pp, c2)
+        assert torch.equal(c2, counts)
+        s2 = torch.empty(Pp, device=dev)
+        vp = torch.zeros(_native.sign_words(Pp), dtype=torch.int64, device=dev)
+        _native.sign_from_counts(c2, Pp, s2, vp)
+        assert same_bits(s2.cpu().numpy()[:P], vote)
+        assert np.array_equal(vp.cpu().numpy().view(np.uint64)[: osign.pack_planes(vote).size],
+                              osign.pack_planes(np.pad(vote, (0, Pp - P))))
+
+
+@pytest.mark.parametrize("K", [1, 2, 15, 16, 255, 256, 1023, 1024, 4100])
+def test_vote_counter_widths(K):
+    """Every bit-sliced counter width, including K at each 2^B boundary."""
+    from distributed_learning_simulator_amd import _native
+    P = 1024
+    g = torch.Generator(device=dev).manual_seed(K)
+    planes = torch.randint(-2**62, 2**62, (K, _native.sign_words(P)), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]  # no NaN codes
+    planes[: K // 2 + 1, 0::2] |= -1  # a majority positive on every parameter...
+    planes[: K // 2 + 1, 1::2] = 0
+    counts = torch.empty(P, dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, None, K, P, counts)
+    w = planes.cpu().numpy().view(np.uint64)
+    ref = np.zeros(P, np.int64)
+    for k in range(K):
+        ref += osign.unpack_planes(w[k], P).astype(np.int64)
+    assert np.array_equal(counts.cpu().numpy(), ref)
+
+
+def test_vote_rows_subset_order_free():
+    from distributed_learning_simulator_amd import _native
+    K, P = 40, 2048
+    g = torch.Generator(device=dev).manual_seed(1)
+    S = torch.randint(-1, 2, (K, P), generator=g, device=dev).float()
+    planes, _ = pack(S.cpu().numpy())
+    rows = torch.tensor([5, 3, 39, 0, 12], dtype=torch.int32, device=dev)
+    out = torch.empty(P, device=dev)
+    _native.sign_vote(planes, rows, 5, P, out)
+    ref = osign.majority_vote(S.cpu().numpy()[[5, 3, 39, 0, 12]])
+    assert same_bits(out.cpu().numpy(), ref)
+
+
+def test_vote_1000_clients_resnet18_sampled():
+    """Config 3 at full size: 1000 x 11,173,962 parameters; sampled exact check + linearity."""
+    from distributed_learning_simulator_amd import _native
+    K, P = 1000, 11173962
+    Pp = (P + 3) // 4 * 4
+    W = _native.sign_words(P)
+    g = torch.Generator(device=dev).manual_seed(7)
+    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]
+    counts = torch.empty(Pp, dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, None, K, Pp, counts)
+    # linearity: counts(all) == counts(first half) + counts(second half)
+    c1 = torch.empty_like(counts)
+    c2 = torch.empty_like(counts)
+    _native.sign_vote_count(planes[:500], None, 500, Pp, c1)
+    _native.sign_vote_count(planes[500:], None, 500, Pp, c2)
+    assert torch.equal(counts, c1 + c2)
+    # exact check on 2048 sampled parameters
+    idx = torch.randint(0, P, (2048,), generator=g, device=dev)
+    words = planes[:, (idx // 64) * 2].cpu().numpy().view(np.uint64)
+    nwords = planes[:, (idx // 64) * 2 + 1].cpu().numpy().view(np.uint64)
+    bit = (idx % 64).cpu().numpy().astype(np.uint64)
+    pos = ((words >> bit) & np.uint64(1)).astype(np.int64).sum(0)
+    neg = ((nwords >> bit) & np.uint64(1)).astype(np.int64).sum(0)
+    assert np.array_equal(counts[idx].cpu().numpy(), pos - neg)
+
+
+def test_sign_worker_golden_bit_exact():
+    """workers/sign_sgd_worker.py:19-58 fused on device, step by step vs golden."""
+    from distributed_learning_simulator_amd import _native
+    z = G.load("sign_worker.npz")
+    for case in G.meta(z):
+        k, cfg, layout = case["key"], case["cfg"], case["layout"]
+        p = torch.from_numpy(z[f"{k}_p0"].copy())
+        bufs, seen = {}, set()
+        for s in range(case["steps"]):
+            grad, has = z[f"{k}_s{s}_grad"], z[f"{k}_s{s}_hasgrad"]
+            vote = z[f"{k}_s{s}_vote"]
+            off = 0
+            newp = p.clone()
+            for ti, (name, shape) in enumerate(layout):
+                m = int(np.prod(shape))
+                sl = slice(off, off + m)
+                off += m
+                if not has[ti]:
+                    continue
+                first = name not in seen
+                gd = torch.from_numpy(grad[sl].copy()).to(dev)
+                if name not in bufs:
+                    bufs[name] = torch.zeros(m, device=dev)
+                planes = torch.zeros(_native.sign_words(m), dtype=torch.int64, device=dev)
+                sout = torch.empty(m, device=dev)
+                _native.sign_sgd_direction(gd, bufs[name], cfg["momentum"], 1 - cfg["dampening"],
+                                           cfg["nesterov"], first, planes, sout)
+                if cfg["momentum"] != 0:
+                    seen.add(name)
+                    assert same_bits(bufs[name].cpu().numpy(), z[f"{k}_s{s}_buf"][sl])
+                assert same_bits(sout.cpu().numpy(), z[f"{k}_s{s}_sent"][sl]), (k, s, name)
+                vplanes = torch.from_numpy(osign.pack_planes(vote[sl]).view(np.int64)).to(dev)
+                pd = p[sl].clone().to(dev)
+                _native.sign_sgd_apply(pd, vplanes, -cfg["lr"], cfg["weight_decay"])
+                newp[sl] = pd.cpu()
+            p = newp
+            assert same_bits(p.numpy(), z[f"{k}_s{s}_param"]), (k, s)

@@ -76,16 +76,19 @@ def test_sign_pack_layout_roundtrip():
     x = np.sign(rng.standard_normal(1000)).astype(np.float32)
     x[::17] = 0
     x[5] = np.nan
-    planes = sign.pack_planes(x).reshape(-1, 4, 2)
-    for p in (0, 1, 2, 3, 4, 255, 256, 511, 999):
-        t, r = divmod(p, 256)
-        l, c = divmod(r, 4)
-        pos = (int(planes[t, c, 0]) >> l) & 1
-        neg = (int(planes[t, c, 1]) >> l) & 1
+    planes = sign.pack_planes(x)
+    assert planes.size == 4 * 8
+    w = planes.reshape(-1, 2)
+    for p in (0, 1, 2, 3, 4, 63, 64, 255, 256, 511, 999):
+        g, j = divmod(p, 64)
+        pos = (int(w[g, 0]) >> j) & 1
+        neg = (int(w[g, 1]) >> j) & 1
         if np.isnan(x[p]):
             assert pos == 1 and neg == 1
         else:
             assert pos == int(x[p] > 0) and neg == int(x[p] < 0)
+    assert same_bits(sign.unpack_planes(planes, 1000), x)
+    assert np.all(w[1000 // 64 + 1:] == 0) and (int(w[15, 0]) >> 40) == 0
 
 
 def test_sign_worker_bit_exact():
