@@ -218,7 +218,7 @@ def bench_quant(args, dev):
     store.sz[:, :, 1].zero_()
     rows = list(range(K))
     store._free = []
-    n = torch.randint(100, 1001, (K,), generator=g).tolist()
+    n = torch.randint(100, 1001, (K,), generator=g, device=dev).tolist()
     out = torch.empty(store.layout.P, device=dev)
     rows_t = torch.tensor(rows, dtype=torch.int32, device=dev)
     w_t = torch.tensor(n, dtype=torch.float32, device=dev)

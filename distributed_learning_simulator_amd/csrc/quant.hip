@@ -24,6 +24,79 @@ __device__ __forceinline__ bool scale_fast(float sw) {
     return sw >= 0x1p-59f && sw <= 0x1p50f;
 }
 
+// One client's contribution to a lane's 16 consecutive elements.  TWO: the
+// chunk straddles a channel boundary at `split` (elements [split,16) use the
+// next channel's (scale, zero point)); FIRST: assign instead of accumulate
+// (servers/fed_server.py:62-65).  The exact-division fast path is decided once
+// per client from the channel scale (scale_fast), not per element.
+template <bool SIGNED, bool TWO, bool FIRST>
+__device__ __forceinline__ void accum16(float (&acc)[16], u32x4 qv, f32x2 a, f32x2 b, float wk,
+                                        int split, const FastDiv &d) {
+    if (SIGNED) qv ^= 0x80808080u;  // int8 q read as the unsigned byte q + 128
+    const float zadj = SIGNED ? 128.f : 0.f;
+    const float za = a.y + zadj, zb = b.y + zadj;
+    const bool fast = d.fast && scale_fast(a.x * wk) && (!TWO || scale_fast(b.x * wk));
+    if (__builtin_expect(fast, 1)) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const bool second = TWO && j >= split;
+            const float s = second ? b.x : a.x;
+            const float z = second ? zb : za;
+            const float x = byte_f32(qv[j >> 2], j & 3);
+            const float q = markstein(((x - z) * s) * wk, d.b, d.y);
+            acc[j] = FIRST ? q : acc[j] + q;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const bool second = TWO && j >= split;
+            const float s = second ? b.x : a.x;
+            const float z = second ? zb : za;
+            const float x = byte_f32(qv[j >> 2], j & 3);
+            const float q = (((x - z) * s) * wk) / d.b;
+            acc[j] = FIRST ? q : acc[j] + q;
+        }
+    }
+}
+
+template <bool SIGNED, bool TWO>
+__device__ __forceinline__ void int_chunk_loop(float (&acc)[16], const uint8_t *__restrict__ Qt,
+                                               int64_t ldq, const f32x2 *__restrict__ szc,
+                                               int64_t ldc, const int32_t *__restrict__ rows,
+                                               const float *__restrict__ w, int K, int split,
+                                               const FastDiv &d) {
+    constexpr int U = 4;  // clients in flight per lane
+    const f32x2 zero2 = f32x2{0.f, 0.f};
+    {
+        const int64_t row = rows[0];
+        const u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
+        const f32x2 a = szc[row * ldc];
+        const f32x2 b = TWO ? szc[row * ldc + 1] : zero2;
+        accum16<SIGNED, TWO, true>(acc, qv, a, b, w[0], split, d);
+    }
+    int k = 1;
+    for (; k + U <= K; k += U) {
+        u32x4 qv[U];
+        f32x2 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = rows[k + u];
+            qv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
+            a[u] = szc[row * ldc];
+            b[u] = TWO ? szc[row * ldc + 1] : zero2;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) accum16<SIGNED, TWO, false>(acc, qv[u], a[u], b[u], w[k + u], split, d);
+    }
+    for (; k < K; ++k) {
+        const int64_t row = rows[k];
+        const u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
+        const f32x2 a = szc[row * ldc];
+        const f32x2 b = TWO ? szc[row * ldc + 1] : zero2;
+        accum16<SIGNED, TWO, false>(acc, qv, a, b, w[k], split, d);
+    }
+}
+
 // Integer (per-channel) tile: 16 consecutive elements per lane.
 template <bool SIGNED>
 __device__ __forceinline__ void int_tile(const dls_qtile &t, const uint8_t *__restrict__ Q,
@@ -34,33 +107,16 @@ __device__ __forceinline__ void int_tile(const dls_qtile &t, const uint8_t *__re
     const int p = t.row_pos + e0;
     const int c = t.chan0 + p / t.row_len;
     const int r = p % t.row_len;
-    const float zadj = SIGNED ? 128.f : 0.f;  // int8 bytes are read as (q ^ 0x80) = q + 128
     float acc[16];
     if (t.row_len >= 16) {
         const int split = t.row_len - r;  // elements [0, split) in channel c, rest in c + 1
-        for (int k = 0; k < K; ++k) {
-            const int64_t row = rows[k];
-            u32x4 qv = __builtin_nontemporal_load(
-                reinterpret_cast<const u32x4 *>(Q + row * ldq + t.src + e0));
-            if (SIGNED) qv ^= 0x80808080u;
-            const f32x2 a = sz[row * ldc + c];
-            const f32x2 b = sz[row * ldc + c + 1];
-            const float wk = w[k];
-            const float za = a.y + zadj, zb = b.y + zadj;
-            const bool fast = d.fast && scale_fast(a.x * wk) && scale_fast(b.x * wk);
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const bool second = j >= split;
-                const float s = second ? b.x : a.x;
-                const float z = second ? zb : za;
-                const float x = byte_f32(qv[j >> 2], j & 3);
-                const float deq = (x - z) * s;
-                const float tn = deq * wk;
-                const float q = fast ? markstein(tn, d.b, d.y) : tn / d.b;
-                acc[j] = (k == 0) ? q : acc[j] + q;
-            }
-        }
+        // wave-uniform choice: most waves of a large-row tensor never straddle a channel
+        if (__ballot(split < 16) == 0)
+            int_chunk_loop<SIGNED, false>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K, 16, d);
+        else
+            int_chunk_loop<SIGNED, true>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K, split, d);
     } else {  // tiny channel rows: per-element channel lookup
+        const float zadj = SIGNED ? 128.f : 0.f;
         int cj[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) cj[j] = min(c + (r + j) / t.row_len, t.chan_end - 1);

@@ -37,14 +37,14 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                                                         float *__restrict__ out, int64_t ldo,
                                                         int64_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int Kp = (K + 1) & ~1;
+    const int Kp = (K + 7) & ~7;  // k-steps of 2 clients, 4 steps per pipeline round
     float *Ct = smem;                                        // [Kp][32*MT]
     int32_t *srow = reinterpret_cast<int32_t *>(smem + Kp * 32 * MT);  // [Kp]
     for (int idx = threadIdx.x; idx < Kp * 32 * MT; idx += kBlock) {
         const int k = idx / (32 * MT), i = idx % (32 * MT);
         Ct[idx] = (k < K && i < S) ? C[(int64_t)i * ldc + k] : 0.f;
     }
-    for (int k = threadIdx.x; k < Kp; k += kBlock) srow[k] = k < K ? rows[k] : -1;
+    for (int k = threadIdx.x; k < Kp + 8; k += kBlock) srow[k] = k < K ? rows[k] : -1;
     __syncthreads();
 
     const int lane = __lane_id();
@@ -71,13 +71,18 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                 }
             }
         }
-#pragma unroll 4
-        for (int s = 0; s < Kp / 2; ++s) {
-            const int k = 2 * s + h;
-            const int32_t r = srow[k];
+        // software pipeline: the U loads of the next 4 k-steps are in flight while
+        // the MFMAs of the current one run (named registers, no runtime indexing)
+        auto loadB = [&](int s) -> f32x4 {
+            const int32_t r = srow[2 * s + h];
             f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
             if (r >= 0 && inb)
-                b = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + p));
+                b = __builtin_nontemporal_load(
+                    reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + p));
+            return b;
+        };
+        auto mma = [&](int s, const f32x4 &b) {
+            const int k = 2 * s + h;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const float a = Ct[k * 32 * MT + 32 * mt + col];
@@ -85,6 +90,18 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                 for (int n = 0; n < 4; ++n)
                     acc[mt][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[n], acc[mt][n], 0, 0, 0);
             }
+        };
+        const int nsteps = Kp / 2;  // multiple of 4 (Kp padded to 8)
+        f32x4 b0 = loadB(0), b1 = loadB(1), b2 = loadB(2), b3 = loadB(3);
+        for (int s = 0; s < nsteps; s += 4) {
+            mma(s, b0);
+            b0 = loadB(s + 4);
+            mma(s + 1, b1);
+            b1 = loadB(s + 5);
+            mma(s + 2, b2);
+            b2 = loadB(s + 6);
+            mma(s + 3, b3);
+            b3 = loadB(s + 7);
         }
         if (inb) {
 #pragma unroll
@@ -123,9 +140,9 @@ extern "C" int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const f
         const int Sc = S - s0 < 64 ? S - s0 : 64;
         for (int k0 = 0; k0 < K; k0 += kMaxK) {
             const int Kc = K - k0 < kMaxK ? K - k0 : kMaxK;
-            const int Kp = (Kc + 1) & ~1;
+            const int Kp = (Kc + 7) & ~7;
             const int MT = Sc > 32 ? 2 : 1;
-            const size_t lds = (size_t)Kp * 32 * MT * sizeof(float) + (size_t)Kp * sizeof(int32_t);
+            const size_t lds = (size_t)Kp * 32 * MT * sizeof(float) + (size_t)(Kp + 8) * sizeof(int32_t);
             // C chunk: rows s0.., columns k0.. of the row-major [S, K] matrix (ld K)
             const float *Cc = C + (int64_t)s0 * K + k0;
             const int beta = k0 > 0;

@@ -6,9 +6,10 @@
 //
 // Vote (servers/sign_sgd_server.py:12-21): counts = #pos - #neg per parameter,
 // accumulated with bit-sliced ("vertical") counters: one 64-bit word per
-// counter bit holds that bit of 64 parameters' counts, so one client costs
-// 2 x B bitwise ops per plane word (B = ceil(log2(K+1))) and no per-parameter
-// unpacking; the counters are unpacked once at the end.  Exact in any order.
+// counter bit holds that bit of 64 parameters' counts, fed by a carry-save
+// (Harley-Seal) adder tree, so 16 clients cost 15 CSAs (5 bitwise ops each)
+// per plane word and no per-parameter unpacking; the counters are unpacked
+// once at the end.  Exact in any order.
 #include "dls_common.h"
 
 namespace dls {
@@ -27,39 +28,29 @@ __device__ __forceinline__ uint64_t spread16(uint64_t x) {
 }
 
 // One wavefront packs one 256-parameter tile: lane l loads parameters 4l..4l+3
-// (16 B), one 64-lane ballot per component gives bit l = parameter 4l + c, and
-// a scalar 4-way bit interleave turns the four ballots into the natural order.
-__device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile,
-                                          int32_t *nonternary) {
+// (16 B); one 64-lane ballot per component c gives bit l = parameter 4l + c.
+// Output word m (parameters 64m..64m+63) takes bit j from ballot_{j&3} bit
+// 16m + (j>>2): lanes 0..7 each build one word (m = lane/2, pos/neg = lane&1)
+// with a 4-way bit interleave in VALU, in parallel.
+__device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *nonternary) {
     const int lane = __lane_id();
     uint64_t pos[4], neg[4];
-    int bad = 0;
+    int nbad = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const float x = v[c];
         const bool nan = x != x;
         pos[c] = __ballot(x > 0.f || nan);
         neg[c] = __ballot(x < 0.f || nan);
-        bad |= !(x == 0.f || x == 1.f || x == -1.f || nan);
+        if (nonternary) nbad += __popcll(__ballot(!(x == 0.f || x == 1.f || x == -1.f || nan)));
     }
-    if (nonternary) {
-        const uint64_t b = __ballot(bad);
-        if (b && lane == 0) atomicAdd(nonternary, (int)__popcll(b));
-    }
-    // word m: bit j <- ballot_{j&3} bit (16m + (j>>2)); wave-uniform (scalar) math
-    uint64_t words[8];
+    if (nonternary && nbad && lane == 0) atomicAdd(nonternary, nbad);
+    const int m = (lane >> 1) & 3;
+    const bool isneg = lane & 1;
+    uint64_t w = 0;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        words[2 * m] = spread16(pos[0] >> (16 * m)) | (spread16(pos[1] >> (16 * m)) << 1) |
-                       (spread16(pos[2] >> (16 * m)) << 2) | (spread16(pos[3] >> (16 * m)) << 3);
-        words[2 * m + 1] = spread16(neg[0] >> (16 * m)) | (spread16(neg[1] >> (16 * m)) << 1) |
-                           (spread16(neg[2] >> (16 * m)) << 2) |
-                           (spread16(neg[3] >> (16 * m)) << 3);
-    }
-    uint64_t mine = words[0];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) mine = (lane == q) ? words[q] : mine;
-    if (lane < 8) dst_tile[lane] = mine;
+    for (int c = 0; c < 4; ++c) w |= spread16((isneg ? neg[c] : pos[c]) >> (16 * m)) << c;
+    if (lane < 8) dst_tile[lane] = w;
 }
 
 // grid: x = tile blocks (4 tiles per block), y = client.
@@ -75,7 +66,7 @@ __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ 
     const float *row = X + k * ldx;
     f32x4 v;
     if (e + 4 <= P) {
-        v = *reinterpret_cast<const f32x4 *>(row + e);
+        v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(row + e));
     } else {
         v = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int c = 0; c < 4; ++c)
@@ -85,28 +76,61 @@ __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ 
 }
 
 // ---------------------------------------------------------------- vote
-// Bit-sliced increment: c += x (x one bit per parameter).
-template <int B>
-__device__ __forceinline__ void vinc(uint64_t (&c)[B], uint64_t x) {
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        const uint64_t t = c[b] & x;
-        c[b] ^= x;
-        x = t;
-    }
+// Carry-save (Harley-Seal) accumulation of 16 one-bit planes: ones/twos/fours/
+// eights are carry-save partial counts, every 16 inputs emit a "sixteens" word
+// that ripples into the CB-bit counter c (in units of 16).  15 CSAs of 5 ops
+// per 16 clients instead of 16 ripple increments of 2*B ops.
+__device__ __forceinline__ void csa(uint64_t &h, uint64_t &l, uint64_t a, uint64_t b, uint64_t c) {
+    const uint64_t u = a ^ b;
+    h = (a & b) | (u & c);
+    l = u ^ c;
 }
 
-template <int B>
-__device__ __forceinline__ int unpack_count(const uint64_t (&c)[B], int j) {
-    int v = 0;
+template <int CB>
+struct HSCounter {
+    uint64_t ones = 0, twos = 0, fours = 0, eights = 0;
+    uint64_t c[CB];
+    __device__ __forceinline__ HSCounter() {
 #pragma unroll
-    for (int b = 0; b < B; ++b) v |= (int)((c[b] >> j) & 1u) << b;
-    return v;
-}
+        for (int b = 0; b < CB; ++b) c[b] = 0;
+    }
+    __device__ __forceinline__ void add16(const uint64_t (&x)[16]) {
+        uint64_t twosA, twosB, foursA, foursB, eightsA, eightsB, sixteens;
+        csa(twosA, ones, ones, x[0], x[1]);
+        csa(twosB, ones, ones, x[2], x[3]);
+        csa(foursA, twos, twos, twosA, twosB);
+        csa(twosA, ones, ones, x[4], x[5]);
+        csa(twosB, ones, ones, x[6], x[7]);
+        csa(foursB, twos, twos, twosA, twosB);
+        csa(eightsA, fours, fours, foursA, foursB);
+        csa(twosA, ones, ones, x[8], x[9]);
+        csa(twosB, ones, ones, x[10], x[11]);
+        csa(foursA, twos, twos, twosA, twosB);
+        csa(twosA, ones, ones, x[12], x[13]);
+        csa(twosB, ones, ones, x[14], x[15]);
+        csa(foursB, twos, twos, twosA, twosB);
+        csa(eightsB, fours, fours, foursA, foursB);
+        csa(sixteens, eights, eights, eightsA, eightsB);
+#pragma unroll
+        for (int b = 0; b < CB; ++b) {  // c += sixteens (bit-sliced ripple)
+            const uint64_t t = c[b] & sixteens;
+            c[b] ^= sixteens;
+            sixteens = t;
+        }
+    }
+    __device__ __forceinline__ int count(int j) const {
+        int v = (int)((ones >> j) & 1u) | ((int)((twos >> j) & 1u) << 1) |
+                ((int)((fours >> j) & 1u) << 2) | ((int)((eights >> j) & 1u) << 3);
+#pragma unroll
+        for (int b = 0; b < CB; ++b) v |= (int)((c[b] >> j) & 1u) << (4 + b);
+        return v;
+    }
+};
 
 // One lane owns one group of 64 parameters (one 16-byte [pos, neg] load per
-// client).  Outputs: counts (int32, optional) and/or fp32 signs.
-template <int B, int UNROLL>
+// client, 16 clients in flight).  Outputs: counts (int32, optional) and/or
+// fp32 signs.  Exact: the counters hold K < 16 * 2^CB.
+template <int CB>
 __global__ __launch_bounds__(kBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
                                                       int64_t ldp, const int32_t *__restrict__ rows,
                                                       int K, int64_t P, int64_t ngroups,
@@ -114,33 +138,40 @@ __global__ __launch_bounds__(kBlock) void k_sign_vote(const uint64_t *__restrict
                                                       float *__restrict__ sign_out) {
     const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (g >= ngroups) return;
-    uint64_t cp[B], cn[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) cp[b] = cn[b] = 0;
+    HSCounter<CB> cp, cn;
     uint64_t nan = 0;
     const u64x2 *base = reinterpret_cast<const u64x2 *>(planes) + g;
     const int64_t ldp2 = ldp / 2;
-    int j = 0;
-    for (; j + UNROLL <= K; j += UNROLL) {
-        u64x2 w[UNROLL];
+    for (int j = 0; j < K; j += 16) {
+        uint64_t xp[16], xn[16];
+        if (j + 16 <= K) {
+            u64x2 w[16];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const int64_t r = rows ? rows[j + u] : (j + u);
-            w[u] = __builtin_nontemporal_load(base + r * ldp2);
+            for (int u = 0; u < 16; ++u) {
+                const int64_t r = rows ? rows[j + u] : (j + u);
+                w[u] = __builtin_nontemporal_load(base + r * ldp2);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                xp[u] = w[u][0];
+                xn[u] = w[u][1];
+            }
+        } else {  // tail: missing clients count as zero planes
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                xp[u] = xn[u] = 0;
+                if (j + u < K) {
+                    const int64_t r = rows ? rows[j + u] : (j + u);
+                    const u64x2 w = base[r * ldp2];
+                    xp[u] = w[0];
+                    xn[u] = w[1];
+                }
+            }
         }
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            nan |= w[u][0] & w[u][1];
-            vinc<B>(cp, w[u][0]);
-            vinc<B>(cn, w[u][1]);
-        }
-    }
-    for (; j < K; ++j) {
-        const int64_t r = rows ? rows[j] : j;
-        const u64x2 w = __builtin_nontemporal_load(base + r * ldp2);
-        nan |= w[0] & w[1];
-        vinc<B>(cp, w[0]);
-        vinc<B>(cn, w[1]);
+        for (int u = 0; u < 16; ++u) nan |= xp[u] & xn[u];
+        cp.add16(xp);
+        cn.add16(xn);
     }
     const int64_t e0 = g * 64;
     const bool full = e0 + 64 <= P;
@@ -151,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_sign_vote(const uint64_t *__restrict
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int jbit = 4 * q + t;
-            int c = unpack_count<B>(cp, jbit) - unpack_count<B>(cn, jbit);
+            int c = cp.count(jbit) - cn.count(jbit);
             const bool poisoned = (nan >> jbit) & 1u;
             if (poisoned) c += DLS_SIGN_NAN_MARK;
             c4[t] = c;
@@ -277,25 +308,26 @@ __global__ __launch_bounds__(kBlock) void k_sign_sgd_apply(float *__restrict__ p
     }
 }
 
-template <int B>
+template <int CB>
 int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K, int64_t P,
                 int32_t *counts, float *sign_out, hipStream_t st) {
     const int64_t ngroups = (P + 63) / 64;
     const dim3 grid((unsigned)((ngroups + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL((k_sign_vote<B, 8>), grid, dim3(kBlock), 0, st, planes, ldp, rows, K, P,
+    hipLaunchKernelGGL((k_sign_vote<CB>), grid, dim3(kBlock), 0, st, planes, ldp, rows, K, P,
                        ngroups, counts, sign_out);
     return check_launch("dls_sign_vote");
 }
 
 int vote_dispatch(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K, int64_t P,
                   int32_t *counts, float *sign_out, hipStream_t st) {
-    // counter width B: K <= 2^B - 1 (fewer bits = fewer ops and registers)
-    if (K < (1 << 4)) return launch_vote<4>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (K < (1 << 8)) return launch_vote<8>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (K < (1 << 10)) return launch_vote<10>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (K < (1 << 12)) return launch_vote<12>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (K < (1 << 16)) return launch_vote<16>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (K < (1 << 20)) return launch_vote<20>(planes, ldp, rows, K, P, counts, sign_out, st);
+    // counts reach 16*c + 15 with c <= ceil(K/16) < 2^CB (fewer bits = fewer ops/registers)
+    const int64_t c_max = (K + 15) / 16;
+    if (c_max < (1 << 2)) return launch_vote<2>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (c_max < (1 << 4)) return launch_vote<4>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (c_max < (1 << 6)) return launch_vote<6>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (c_max < (1 << 8)) return launch_vote<8>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (c_max < (1 << 12)) return launch_vote<12>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (K < (1 << 20)) return launch_vote<16>(planes, ldp, rows, K, P, counts, sign_out, st);
     set_error("dls_sign_vote: K=%d exceeds 2^20-1 clients", K);
     return DLS_EINVAL;
 }
