@@ -60,8 +60,9 @@ SIGNATURES = {
     "dls_dequant_fedavg": ([_p, _i32, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i32, _f32, _p, _p],
                            _i32),
     "dls_segment_minmax_f32": ([_p, _p, _i32, _p, _p, _i64, _p], _i32),
-    "dls_qparams_minmax": ([_p, _p, _i32, _i32, _i32, _p, _p, _p], _i32),
-    "dls_quantize_u8": ([_p, _p, _i32, _p, _p, _p, _p, _i32, _u64, _i64, _p], _i32),
+    "dls_qparams_minmax": ([_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p], _i32),
+    "dls_quantize_affine": ([_p, _p, _i32, _p, _p, _i32, _i32, _p, _p, _i32, _u64, _i64, _p],
+                            _i32),
 }
 
 _lib = None
@@ -101,9 +102,13 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _stream(stream=None):
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return ctypes.c_void_p(s.cuda_stream)
+def _stream(stream=None, like=None):
+    """The given stream, else the current stream of `like`'s device (worker threads
+    may run with another current device than the tensors they launch on)."""
+    if stream is None:
+        dev = like.device if like is not None and like.is_cuda else None
+        stream = torch.cuda.current_stream(dev)
+    return ctypes.c_void_p(stream.cuda_stream)
 
 
 def require_gpu():
@@ -118,7 +123,7 @@ def fedavg(U, rows, weight, total, P, out, mode=FEDAVG_EXACT, stream=None):
     assert U.dtype == torch.float32 and out.dtype == torch.float32
     assert rows.dtype == torch.int32 and weight.dtype == torch.float32
     _check(lib().dls_fedavg_f32(_ptr(U), U.stride(0), _ptr(rows), _ptr(weight), rows.numel(),
-                                float(total), P, mode, _ptr(out), _stream(stream)),
+                                float(total), P, mode, _ptr(out), _stream(stream, U)),
            "dls_fedavg_f32")
     return out
 
@@ -127,7 +132,7 @@ def subset_fedavg(U, sub_off, sub_rows, sub_weight, sub_total, P, out, stream=No
     S = sub_off.numel() - 1
     _check(lib().dls_subset_fedavg_f32(_ptr(U), U.stride(0), _ptr(sub_off), _ptr(sub_rows),
                                        _ptr(sub_weight), _ptr(sub_total), S, P, _ptr(out),
-                                       out.stride(0), _stream(stream)), "dls_subset_fedavg_f32")
+                                       out.stride(0), _stream(stream, U)), "dls_subset_fedavg_f32")
     return out
 
 
@@ -135,7 +140,7 @@ def subset_gemm(C, U, rows, P, out, stream=None):
     S, K = C.shape
     assert C.is_contiguous() and C.dtype == torch.float32
     _check(lib().dls_subset_gemm_f32(_ptr(C), S, K, _ptr(U), U.stride(0), _ptr(rows), P, _ptr(out),
-                                     out.stride(0), _stream(stream)), "dls_subset_gemm_f32")
+                                     out.stride(0), _stream(stream, U)), "dls_subset_gemm_f32")
     return out
 
 
@@ -143,24 +148,24 @@ def subset_gemm(C, U, rows, P, out, stream=None):
 def sign_pack(X, P, planes, nonternary=None, stream=None):
     K = X.shape[0]
     _check(lib().dls_sign_pack_f32(_ptr(X), X.stride(0), K, P, _ptr(planes), planes.stride(0),
-                                   _ptr(nonternary), _stream(stream)), "dls_sign_pack_f32")
+                                   _ptr(nonternary), _stream(stream, X)), "dls_sign_pack_f32")
     return planes
 
 
 def sign_vote_count(planes, rows, K, P, counts, stream=None):
     _check(lib().dls_sign_vote_count(_ptr(planes), planes.stride(0), _ptr(rows), K, P,
-                                     _ptr(counts), _stream(stream)), "dls_sign_vote_count")
+                                     _ptr(counts), _stream(stream, planes)), "dls_sign_vote_count")
     return counts
 
 
 def sign_from_counts(counts, P, sign_out=None, vote_planes=None, stream=None):
     _check(lib().dls_sign_from_counts(_ptr(counts), P, _ptr(sign_out), _ptr(vote_planes),
-                                      _stream(stream)), "dls_sign_from_counts")
+                                      _stream(stream, counts)), "dls_sign_from_counts")
 
 
 def sign_vote(planes, rows, K, P, sign_out, counts=None, stream=None):
     _check(lib().dls_sign_vote(_ptr(planes), planes.stride(0), _ptr(rows), K, P, _ptr(counts),
-                               _ptr(sign_out), _stream(stream)), "dls_sign_vote")
+                               _ptr(sign_out), _stream(stream, planes)), "dls_sign_vote")
     return sign_out
 
 
@@ -170,12 +175,12 @@ def sign_sgd_direction(grad, buf, momentum, one_minus_dampening, nesterov, first
     _check(lib().dls_sign_sgd_direction(_ptr(grad), _ptr(buf), P, float(momentum),
                                         float(one_minus_dampening), int(bool(nesterov)),
                                         int(bool(first)), _ptr(planes), _ptr(sign_out),
-                                        _stream(stream)), "dls_sign_sgd_direction")
+                                        _stream(stream, grad)), "dls_sign_sgd_direction")
 
 
 def sign_sgd_apply(param, vote_planes, neg_lr, weight_decay, stream=None):
     _check(lib().dls_sign_sgd_apply(_ptr(param), _ptr(vote_planes), param.numel(), float(neg_lr),
-                                    float(weight_decay), _stream(stream)), "dls_sign_sgd_apply")
+                                    float(weight_decay), _stream(stream, param)), "dls_sign_sgd_apply")
 
 
 # ----------------------------------------------------------------------- quant
@@ -184,24 +189,31 @@ def dequant_fedavg(tiles, ntiles, Q, F, sz, rows, weight, total, out, stream=Non
                                     _ptr(F), F.stride(0) if F is not None else 0, _ptr(sz),
                                     sz.stride(0) // 2, _ptr(rows),
                                     _ptr(weight), rows.numel(), float(total), _ptr(out),
-                                    _stream(stream)), "dls_dequant_fedavg")
+                                    _stream(stream, out)), "dls_dequant_fedavg")
     return out
 
 
 def segment_minmax(x, seg_off, total, mins, maxs, stream=None):
     _check(lib().dls_segment_minmax_f32(_ptr(x), _ptr(seg_off), seg_off.numel() - 1, _ptr(mins),
-                                        _ptr(maxs), total, _stream(stream)),
+                                        _ptr(maxs), total, _stream(stream, x)),
            "dls_segment_minmax_f32")
 
 
-def qparams_minmax(mins, maxs, scale, zp, qmin=0, qmax=255, stream=None):
-    _check(lib().dls_qparams_minmax(_ptr(mins), _ptr(maxs), mins.numel(), qmin, qmax, _ptr(scale),
-                                    _ptr(zp), _stream(stream)), "dls_qparams_minmax")
+def qparams_minmax(mins, maxs, scale, zp, qmin=0, qmax=255, symmetric=False, stream=None):
+    _check(lib().dls_qparams_minmax(_ptr(mins), _ptr(maxs), mins.numel(), qmin, qmax,
+                                    int(bool(symmetric)), _ptr(scale), _ptr(zp),
+                                    _stream(stream, mins)), "dls_qparams_minmax")
+
+
+def quantize(x, seg_off, total, scale, zp, q, deq=None, qmin=0, qmax=255, stochastic=False,
+             seed=0, stream=None):
+    _check(lib().dls_quantize_affine(_ptr(x), _ptr(seg_off), seg_off.numel() - 1, _ptr(scale),
+                                     _ptr(zp), qmin, qmax, _ptr(q), _ptr(deq),
+                                     int(bool(stochastic)),
+                                     ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), total,
+                                     _stream(stream, x)), "dls_quantize_affine")
 
 
 def quantize_u8(x, seg_off, total, scale, zp, q, deq=None, stochastic=False, seed=0,
                 stream=None):
-    _check(lib().dls_quantize_u8(_ptr(x), _ptr(seg_off), seg_off.numel() - 1, _ptr(scale),
-                                 _ptr(zp), _ptr(q), _ptr(deq), int(bool(stochastic)),
-                                 ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), total,
-                                 _stream(stream)), "dls_quantize_u8")
+    quantize(x, seg_off, total, scale, zp, q, deq, 0, 255, stochastic, seed, stream)

@@ -296,13 +296,20 @@ __global__ __launch_bounds__(kBlock) void k_segment_minmax(const float *__restri
 }
 
 __global__ void k_qparams(const float *mins, const float *maxs, int nseg, int qmin, int qmax,
-                          float *scale, int32_t *zp) {
+                          int symmetric, float *scale, int32_t *zp) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nseg) return;
-    // torch.ao MinMaxObserver._calculate_qparams (per_tensor_affine), fp32 tensor math
+    // torch.ao MinMaxObserver._calculate_qparams, fp32 tensor math
+    const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
     const float lo = fminf(mins[s], 0.f), hi = fmaxf(maxs[s], 0.f);
+    if (symmetric) {  // per_tensor/per_channel_symmetric
+        float sc = fmaxf(-lo, hi) / ((float)(qmax - qmin) / 2.f);
+        scale[s] = fmaxf(sc, eps);
+        zp[s] = qmin < 0 ? 0 : (qmin + qmax + 1) / 2;
+        return;
+    }
     float sc = (hi - lo) / (float)(qmax - qmin);
-    sc = fmaxf(sc, 1.1920928955078125e-07f);
+    sc = fmaxf(sc, eps);
     float z = (float)qmin - rintf(lo / sc);
     z = fminf(fmaxf(z, (float)qmin), (float)qmax);
     scale[s] = sc;
@@ -318,13 +325,13 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t e) {
     return (float)(uint32_t)(z >> 40) * 0x1p-24f;
 }
 
-__global__ __launch_bounds__(kBlock) void k_quantize_u8(const float *__restrict__ x,
-                                                        const int64_t *__restrict__ seg_off,
-                                                        int nseg, const float *__restrict__ scale,
-                                                        const int32_t *__restrict__ zp,
-                                                        uint8_t *__restrict__ q,
-                                                        float *__restrict__ deq, int stochastic,
-                                                        uint64_t seed) {
+__global__ __launch_bounds__(kBlock) void k_quantize(const float *__restrict__ x,
+                                                     const int64_t *__restrict__ seg_off, int nseg,
+                                                     const float *__restrict__ scale,
+                                                     const int32_t *__restrict__ zp, float qmin,
+                                                     float qmax, uint8_t *__restrict__ q,
+                                                     float *__restrict__ deq, int stochastic,
+                                                     uint64_t seed) {
     __shared__ int s_seg;
     const int64_t total = seg_off[nseg];
     const int64_t e0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
@@ -343,8 +350,8 @@ __global__ __launch_bounds__(kBlock) void k_quantize_u8(const float *__restrict_
         const float z = (float)zp[s];
         const float v = x[e] * inv;
         const float r = stochastic ? floorf(v + uniform01(seed, (uint64_t)e)) : rintf(v);
-        const float qf = fminf(fmaxf(r + z, 0.f), 255.f);  // nan -> 0
-        packed |= (uint32_t)qf << (8 * t);
+        const float qf = fminf(fmaxf(r + z, qmin), qmax);  // nan -> qmin
+        packed |= ((uint32_t)(int32_t)qf & 0xffu) << (8 * t);
         dq[t] = (qf - z) * sc;
     }
     const int64_t n = total - e0 < 4 ? total - e0 : 4;
@@ -395,23 +402,27 @@ extern "C" int dls_segment_minmax_f32(const float *x, const int64_t *seg_off, in
 }
 
 extern "C" int dls_qparams_minmax(const float *mins, const float *maxs, int32_t nseg, int32_t qmin,
-                                  int32_t qmax, float *scale, int32_t *zp, dls_stream_t stream) {
+                                  int32_t qmax, int32_t symmetric, float *scale, int32_t *zp,
+                                  dls_stream_t stream) {
     DLS_REQUIRE(mins && maxs && scale && zp && nseg > 0 && qmax > qmin, DLS_EINVAL,
                 "dls_qparams_minmax: bad arguments");
     hipLaunchKernelGGL(k_qparams, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), mins, maxs, (int)nseg, (int)qmin, (int)qmax, scale, zp);
+                       as_stream(stream), mins, maxs, (int)nseg, (int)qmin, (int)qmax,
+                       (int)symmetric, scale, zp);
     return check_launch("dls_qparams_minmax");
 }
 
-extern "C" int dls_quantize_u8(const float *x, const int64_t *seg_off, int32_t nseg,
-                               const float *scale, const int32_t *zp, uint8_t *q, float *deq,
-                               int32_t stochastic, uint64_t seed, int64_t total,
-                               dls_stream_t stream) {
+extern "C" int dls_quantize_affine(const float *x, const int64_t *seg_off, int32_t nseg,
+                                   const float *scale, const int32_t *zp, int32_t qmin,
+                                   int32_t qmax, void *q, float *deq, int32_t stochastic,
+                                   uint64_t seed, int64_t total, dls_stream_t stream) {
     DLS_REQUIRE(x && seg_off && scale && zp && q && nseg > 0 && total > 0, DLS_EINVAL,
-                "dls_quantize_u8: bad arguments");
+                "dls_quantize_affine: bad arguments");
+    DLS_REQUIRE(qmin >= -128 && qmax <= 255 && qmax > qmin && qmax - qmin <= 255, DLS_EINVAL,
+                "dls_quantize_affine: [qmin, qmax] = [%d, %d] must fit one byte", qmin, qmax);
     const int64_t threads = (total + 3) / 4;
-    hipLaunchKernelGGL(k_quantize_u8, dim3((unsigned)((threads + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, as_stream(stream), x, seg_off, (int)nseg, scale, zp, q, deq,
-                       (int)stochastic, seed);
-    return check_launch("dls_quantize_u8");
+    hipLaunchKernelGGL(k_quantize, dim3((unsigned)((threads + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, as_stream(stream), x, seg_off, (int)nseg, scale, zp, (float)qmin,
+                       (float)qmax, reinterpret_cast<uint8_t *>(q), deq, (int)stochastic, seed);
+    return check_launch("dls_quantize_affine");
 }

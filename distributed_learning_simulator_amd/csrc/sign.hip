@@ -32,7 +32,8 @@ __device__ __forceinline__ uint64_t spread16(uint64_t x) {
 // Output word m (parameters 64m..64m+63) takes bit j from ballot_{j&3} bit
 // 16m + (j>>2): lanes 0..7 each build one word (m = lane/2, pos/neg = lane&1)
 // with a 4-way bit interleave in VALU, in parallel.
-__device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *nonternary) {
+__device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *nonternary,
+                                          int valid_words = 8) {
     const int lane = __lane_id();
     uint64_t pos[4], neg[4];
     int nbad = 0;
@@ -50,7 +51,7 @@ __device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *
     uint64_t w = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) w |= spread16((isneg ? neg[c] : pos[c]) >> (16 * m)) << c;
-    if (lane < 8) dst_tile[lane] = w;
+    if (lane < valid_words) dst_tile[lane] = w;  // a tensor's last tile may end early
 }
 
 // grid: x = tile blocks (4 tiles per block), y = client.
@@ -286,7 +287,8 @@ __global__ __launch_bounds__(kBlock) void k_sign_sgd_direction(
         for (int t = 0; t < 4; ++t)
             if (e + t >= P) s[t] = 0.f;
     }
-    pack_tile(s, planes + tile * 8, nullptr);
+    const int64_t words_left = 2 * ((P + 63) / 64) - tile * 8;
+    pack_tile(s, planes + tile * 8, nullptr, words_left < 8 ? (int)words_left : 8);
 }
 
 // workers/sign_sgd_worker.py:48-57: d = vote (+ fma(p, wd, vote)); p = fma(d, -lr, p).

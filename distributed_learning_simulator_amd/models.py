@@ -1,0 +1,81 @@
+"""Model definitions for the BASELINE configs (random init; no checkpoints).
+
+Parameter names and shapes match ``model_shapes`` (LeNet-5 61,706 params,
+ResNet-18/CIFAR-10 11,173,962 params).  The reference builds its models in the
+absent ``cyy_naive_pytorch_lib``; these standard definitions stand in.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class LeNet5(nn.Module):
+    def __init__(self, num_classes=10):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 6, 5)
+        self.conv2 = nn.Conv2d(6, 16, 5)
+        self.fc1 = nn.Linear(400, 120)
+        self.fc2 = nn.Linear(120, 84)
+        self.fc3 = nn.Linear(84, num_classes)
+
+    def forward(self, x):  # x: [B, 1, 32, 32]
+        x = F.max_pool2d(F.relu(self.conv1(x)), 2)
+        x = F.max_pool2d(F.relu(self.conv2(x)), 2)
+        x = x.flatten(1)
+        return self.fc3(F.relu(self.fc2(F.relu(self.fc1(x)))))
+
+
+class _Block(nn.Module):
+    def __init__(self, cin, cout, stride):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.shortcut = nn.Sequential()
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
+                                          nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return F.relu(out + self.shortcut(x))
+
+
+class ResNet18(nn.Module):
+    """CIFAR-10 ResNet-18 (3x3 stem, no max-pool)."""
+
+    def __init__(self, num_classes=10):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        layers, cin = [], 64
+        for li, cout in enumerate([64, 128, 256, 512]):
+            blocks = []
+            for b in range(2):
+                stride = 2 if (li > 0 and b == 0) else 1
+                blocks.append(_Block(cin, cout, stride))
+                cin = cout
+            layers.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = layers
+        self.linear = nn.Linear(512, num_classes)
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        out = F.adaptive_avg_pool2d(out, 1).flatten(1)
+        return self.linear(out)
+
+
+MODELS = {"LeNet5": LeNet5, "ResNet18": ResNet18}
+
+
+def synthetic_classification(n, shape, num_classes=10, seed=0, noise=1.0):
+    """Learnable synthetic data of the named shape: class templates + Gaussian noise
+    (there is no network access for MNIST / CIFAR-10)."""
+    g = torch.Generator().manual_seed(seed)
+    templates = torch.randn((num_classes,) + tuple(shape), generator=torch.Generator().manual_seed(1234))
+    y = torch.randint(0, num_classes, (n,), generator=g)
+    X = templates[y] + noise * torch.randn((n,) + tuple(shape), generator=g)
+    return X.float(), y

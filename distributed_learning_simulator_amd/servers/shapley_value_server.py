@@ -1,0 +1,64 @@
+"""Shapley-value server base (reference: servers/shapley_value_server.py:9-14).
+
+Adds, on top of the reference's ``powerset``, the batched coalition evaluator
+both Shapley servers use: a batch of S coalitions becomes S subset models in
+one kernel launch (``dls_subset_fedavg_f32``, bit-exact reference order — the
+default, because accuracy utilities are discontinuous — or the fp32 MFMA
+contraction ``dls_subset_gemm_f32`` with ``subset_method="gemm"``), then each
+model is scored with ``get_metric`` (servers/fed_server.py:26-32).  Under
+``torch.distributed`` with several ranks the coalitions are dealt round-robin
+over the ranks and the utilities are summed with one all-reduce (each rank
+fills only its own entries), so every rank ends with the full table.
+"""
+from itertools import chain, combinations
+
+import torch
+import torch.distributed as dist
+
+from .fed_server import FedServer
+
+
+class ShapleyValueServer(FedServer):
+    def __init__(self, subset_method="exact", subset_batch=None, **kwargs):
+        super().__init__(**kwargs)
+        self.subset_method = subset_method
+        self.subset_batch = subset_batch
+        self.evaluated_subsets = []  # coalitions evaluated this round, in evaluation order
+
+    def powerset(self, iterable):
+        "powerset([1,2,3]) --> () (1,) (2,) (3,) (1,2) (1,3) (2,3) (1,2,3)"
+        s = list(iterable)
+        return chain.from_iterable(combinations(s, r) for r in range(len(s) + 1))
+
+    def _batch_size(self):
+        if self.subset_batch:
+            return self.subset_batch
+        P = self.parameters.store.layout.P
+        return max(1, min(64, (2 << 30) // (4 * P)))  # <= 2 GiB of subset models
+
+    def evaluate_subsets(self, subsets):
+        """Utilities of coalitions (tuples of worker ids) -> list of floats, in order."""
+        subsets = [tuple(s) for s in subsets]
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        rank = dist.get_rank() if world > 1 else 0
+        mine = [i for i in range(len(subsets)) if i % world == rank]
+        values = [0.0] * len(subsets)
+        store = self.parameters.store
+        bs = self._batch_size()
+        for b0 in range(0, len(mine), bs):
+            idx = mine[b0:b0 + bs]
+            nonempty = [i for i in idx if subsets[i]]
+            out = None
+            if nonempty:
+                rows = [[self.parameters.row_of(w) for w in subsets[i]] for i in nonempty]
+                out = store.subset_models(rows, self.parameters.n_of_row(), method=self.subset_method)
+            pos = {i: k for k, i in enumerate(nonempty)}
+            for i in idx:
+                model = store.layout.views(out[pos[i]]) if subsets[i] else self.prev_model
+                values[i] = float(self.get_metric(model))
+                self.evaluated_subsets.append(subsets[i])
+        if world > 1:
+            t = torch.tensor(values, dtype=torch.float64, device=self.device)
+            dist.all_reduce(t)
+            values = t.tolist()
+        return values

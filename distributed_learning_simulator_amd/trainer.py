@@ -1,0 +1,139 @@
+"""Minimal trainer / inferencer with the callback surface the reference uses.
+
+The reference drives local training through the absent
+``cyy_naive_pytorch_lib`` Trainer: ``trainer.train()`` runs ``--epoch``
+epochs, fires ``ModelExecutorCallbackPoint.OPTIMIZER_STEP`` callbacks in place
+of ``optimizer.step()`` when registered (workers/sign_sgd_worker.py:15-17) and
+``AFTER_EXECUTE`` callbacks with ``model_executor=trainer`` at the end
+(workers/fed_worker.py:13-17,28-39).  The server's tester exposes
+``inference()``, ``accuracy_metric.get_accuracy(1)`` and
+``loss_metric.get_loss(1)`` (servers/fed_server.py:26-32).  Local training is
+outside the hot path; this is the plumbing config 1 needs.
+"""
+import enum
+
+import torch
+
+
+class ModelExecutorCallbackPoint(enum.Enum):
+    BEFORE_EXECUTE = enum.auto()
+    OPTIMIZER_STEP = enum.auto()
+    AFTER_EXECUTE = enum.auto()
+
+
+class MachineLearningPhase(enum.Enum):
+    Training = enum.auto()
+    Test = enum.auto()
+
+
+class _Accuracy:
+    def __init__(self):
+        self.value = None
+
+    def get_accuracy(self, _epoch=1):
+        return self.value
+
+
+class _Loss:
+    def __init__(self):
+        self.value = None
+
+    def get_loss(self, _epoch=1):
+        return self.value
+
+
+class Inferencer:
+    def __init__(self, model, dataset, batch_size=1024, device=None):
+        self.model = model
+        self.dataset = dataset
+        self.batch_size = batch_size
+        self.device = device or next(model.parameters()).device
+        self.accuracy_metric = _Accuracy()
+        self.loss_metric = _Loss()
+
+    def set_device(self, device):
+        self.device = torch.device(device)
+        self.model.to(self.device)
+
+    @torch.no_grad()
+    def inference(self):
+        X, y = self.dataset
+        self.model.eval()
+        correct, loss_sum = 0, 0.0
+        for i in range(0, X.shape[0], self.batch_size):
+            xb = X[i:i + self.batch_size].to(self.device, non_blocking=True)
+            yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
+            out = self.model(xb)
+            loss_sum += float(torch.nn.functional.cross_entropy(out, yb, reduction="sum"))
+            correct += int((out.argmax(1) == yb).sum())
+        n = X.shape[0]
+        self.accuracy_metric.value = correct / n
+        self.loss_metric.value = torch.tensor(loss_sum / n)
+        return self.loss_metric.value, self.accuracy_metric.value, None
+
+
+class Trainer:
+    def __init__(self, model, dataset, test_dataset=None, epoch=1, batch_size=64,
+                 learning_rate=0.01, momentum=0.0, weight_decay=0.0, optimizer_name="SGD",
+                 device=None, seed=0):
+        self.model = model
+        self.dataset = dataset
+        self.test_dataset = test_dataset
+        self.epoch = epoch
+        self.batch_size = batch_size
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self._callbacks = {p: {} for p in ModelExecutorCallbackPoint}
+        if optimizer_name == "SGD":
+            self._optimizer = torch.optim.SGD(model.parameters(), lr=learning_rate,
+                                              momentum=momentum, weight_decay=weight_decay)
+        elif optimizer_name == "Adam":
+            self._optimizer = torch.optim.Adam(model.parameters(), lr=learning_rate,
+                                               weight_decay=weight_decay)
+        else:
+            raise ValueError(f"unknown optimizer {optimizer_name}")
+        self._gen = torch.Generator().manual_seed(seed)
+
+    def __len__(self):
+        return self.dataset[0].shape[0]
+
+    def set_device(self, device):
+        self.device = torch.device(device)
+        self.model.to(self.device)
+
+    def get_optimizer(self):
+        return self._optimizer
+
+    def add_named_callback(self, point, name, fn):
+        self._callbacks[point][name] = fn
+
+    def get_inferencer(self, phase=MachineLearningPhase.Test, copy_model=False):
+        model = self.model
+        if copy_model:
+            import copy
+            model = copy.deepcopy(model)
+        return Inferencer(model, self.test_dataset, device=self.device)
+
+    def train(self):
+        X, y = self.dataset
+        opt = self._optimizer
+        self.model.to(self.device)
+        for cb in self._callbacks[ModelExecutorCallbackPoint.BEFORE_EXECUTE].values():
+            cb(model_executor=self)
+        for _ in range(self.epoch):
+            self.model.train()
+            perm = torch.randperm(X.shape[0], generator=self._gen)
+            for i in range(0, X.shape[0], self.batch_size):
+                idx = perm[i:i + self.batch_size]
+                xb = X[idx].to(self.device, non_blocking=True)
+                yb = y[idx].to(self.device, non_blocking=True)
+                opt.zero_grad(set_to_none=True)
+                loss = torch.nn.functional.cross_entropy(self.model(xb), yb)
+                loss.backward()
+                steps = self._callbacks[ModelExecutorCallbackPoint.OPTIMIZER_STEP]
+                if steps:
+                    for cb in steps.values():
+                        cb(opt, device=self.device, model_executor=self)
+                else:
+                    opt.step()
+        for cb in self._callbacks[ModelExecutorCallbackPoint.AFTER_EXECUTE].values():
+            cb(model_executor=self)

@@ -117,7 +117,9 @@ int dls_sign_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int3
 
 /* Worker step, workers/sign_sgd_worker.py:32-44 fused: momentum / dampening /
  * nesterov on grad (buf updated in place; first=1 clones), torch.sign, pack to
- * planes (ldp words), optional fp32 sign copy.  a = fl32(1 - dampening). */
+ * planes, optional fp32 sign copy.  a = fl32(1 - dampening).  Writes exactly
+ * 2*ceil(P/64) plane words, so one tensor can fill its slice of a shared row
+ * (tensors start at multiples of 64 parameters). */
 int dls_sign_sgd_direction(const float *grad, float *buf, int64_t P, float momentum,
                            float one_minus_dampening, int32_t nesterov, int32_t first,
                            uint64_t *planes, float *sign_out, dls_stream_t stream);
@@ -160,19 +162,23 @@ int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const void *Q, in
 int dls_segment_minmax_f32(const float *x, const int64_t *seg_off, int32_t nseg, float *mins,
                            float *maxs, int64_t total, dls_stream_t stream);
 
-/* MinMaxObserver-style affine qparams on device (fp32): for each segment
- * scale = max((max(hi,0) - min(lo,0)) / (qmax - qmin), eps),
- * zp = clamp(qmin - rne(min(lo,0) / scale), qmin, qmax). */
+/* MinMaxObserver-style qparams on device (torch.ao _calculate_qparams, fp32):
+ *   affine:    scale = max((max(hi,0) - min(lo,0)) / (qmax - qmin), eps),
+ *              zp = clamp(qmin - rne(min(lo,0) / scale), qmin, qmax);
+ *   symmetric: scale = max(max(-min(lo,0), max(hi,0)) / ((qmax - qmin) / 2), eps),
+ *              zp = 0 (signed range) or (qmin + qmax + 1) / 2 (unsigned). */
 int dls_qparams_minmax(const float *mins, const float *maxs, int32_t nseg, int32_t qmin,
-                       int32_t qmax, float *scale, int32_t *zp, dls_stream_t stream);
+                       int32_t qmax, int32_t symmetric, float *scale, int32_t *zp,
+                       dls_stream_t stream);
 
-/* Affine quantize per segment: q = clamp(rne(x * fl(1/scale)) + zp, 0, 255)
- * (torch quantize_per_tensor); stochastic=1 replaces rne by floor(v + u),
- * u = counter-based uniform(seed, element).  deq (optional) =
- * fl(fl(q - zp) * scale). */
-int dls_quantize_u8(const float *x, const int64_t *seg_off, int32_t nseg, const float *scale,
-                    const int32_t *zp, uint8_t *q, float *deq, int32_t stochastic, uint64_t seed,
-                    int64_t total, dls_stream_t stream);
+/* Affine quantize per segment (torch quantize_per_tensor / _per_channel):
+ * q = clamp(rne(x * fl(1/scale)) + zp, qmin, qmax) stored as one byte (int8 for
+ * qmin < 0, else uint8); stochastic=1 replaces rne by floor(v + u),
+ * u = counter-based uniform(seed, element) (parity unpinned).  deq (optional)
+ * = fl(fl(q - zp) * scale), the client-side dequant formula. */
+int dls_quantize_affine(const float *x, const int64_t *seg_off, int32_t nseg, const float *scale,
+                        const int32_t *zp, int32_t qmin, int32_t qmax, void *q, float *deq,
+                        int32_t stochastic, uint64_t seed, int64_t total, dls_stream_t stream);
 
 #ifdef __cplusplus
 }
