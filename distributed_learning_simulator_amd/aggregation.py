@@ -67,12 +67,16 @@ class ClientUpdateStore:
         return self.layout.views(self.U[row])
 
     # ------------------------------------------------------------ aggregation
-    def fedavg(self, rows, ns, mode=_native.FEDAVG_EXACT, out=None):
-        """Weighted mean of rows in the given order (servers/fed_server.py:44-66)."""
+    def fedavg(self, rows, ns, mode=_native.FEDAVG_EXACT, out=None, total=None):
+        """Weighted mean of rows in the given order (servers/fed_server.py:44-66).
+
+        ``total`` (default: sum of ``ns``) is the divisor N; a shard of a sharded
+        round passes the global N and gets its partial sum."""
         P = self.layout.P
         if out is None:
             out = torch.empty(P, dtype=torch.float32, device=self.device)
-        total = sum(int(n) for n in ns)
+        if total is None:
+            total = sum(int(n) for n in ns)
         _native.fedavg(self.U, _i32(rows, self.device), _f32([int(n) for n in ns], self.device),
                        float(total), P, out, mode=mode)
         return out

@@ -1,0 +1,185 @@
+"""Multi-GPU servers: clients sharded over the GPUs of one node, RCCL exchange.
+
+The reference is one process with one server device (servers/server.py:6-35;
+workers are threads, simulator.py:60-69).  On an MI355X node the hot path
+runs one process per GPU (``torch.distributed`` with the ``nccl`` backend,
+which is RCCL over xGMI on ROCm).  Each rank owns the updates of its own
+clients (``clients_per_round`` = local clients; ``worker_number`` stays the
+global K), aggregates them locally with the same HIP kernels, and one
+collective combines the ranks:
+
+* FedAvg / fed_quant: every rank computes its partial sum with the GLOBAL N
+  (an int64 all-reduce of the local sample counts), then an fp32 SUM
+  all-reduce of the P-element partial, pipelined in chunks so the RCCL
+  transfer of chunk c overlaps the reduction of chunk c+1.  Reference-order
+  within a shard, cross-rank sums in RCCL order: normwise ~1e-7 vs the exact
+  mean (north-star tolerance 1e-6), not bit-exact.
+* sign vote: int32 vote counts per rank, SUM all-reduce, then sign on every
+  rank — bit-exact for any number of ranks.
+
+Client-to-rank placement mirrors the reference's ``worker_id % ngpu``
+(simulator.py:68).
+"""
+import torch
+import torch.distributed as dist
+
+from . import _native
+from .servers.fed_quant_server import FedQuantServer
+from .servers.fed_server import FedServer
+from .servers.sign_sgd_server import SignSGDServer, SignVoteResult
+from .task_queue import RepeatedResult
+
+
+def rank_of_worker(worker_id, world_size):
+    """simulator.py:68 places worker i on device i % ngpu."""
+    return worker_id % world_size
+
+
+def local_workers(worker_number, rank, world_size):
+    return [w for w in range(worker_number) if rank_of_worker(w, world_size) == rank]
+
+
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def global_sample_count(local_ns, device, group=None):
+    t = torch.tensor([sum(int(n) for n in local_ns)], dtype=torch.int64, device=device)
+    if _world()[0] > 1:
+        dist.all_reduce(t, group=group)
+    return int(t.item())
+
+
+def allreduce_chunked(flat, chunks=4, group=None, produce=None):
+    """SUM all-reduce of a flat fp32 vector in ``chunks`` pieces.
+
+    ``produce(c0, c1)`` (optional) fills flat[c0:c1] first; chunk c's all-reduce
+    is issued asynchronously before chunk c+1 is produced, so RCCL over xGMI
+    overlaps the next chunk's reduction kernel."""
+    P = flat.numel()
+    bounds = [P * c // chunks // 256 * 256 for c in range(chunks)] + [P]
+    handles = []
+    for c in range(chunks):
+        c0, c1 = bounds[c], bounds[c + 1]
+        if c1 <= c0:
+            continue
+        if produce is not None:
+            produce(c0, c1)
+        if _world()[0] > 1:
+            handles.append(dist.all_reduce(flat[c0:c1], async_op=True, group=group))
+    for h in handles:
+        h.wait()
+    return flat
+
+
+class _ShardedMixin:
+    def _init_shard(self, worker_number, group, chunks):
+        # before FedServer.__init__, which publishes the initial broadcast to
+        # clients_per_round consumers
+        self.group = group
+        self.chunks = chunks
+        world, rank = _world()
+        self.world_size, self.rank = world, rank
+        self.local_worker_ids = local_workers(worker_number, rank, world)
+
+    @property
+    def clients_per_round(self):
+        return len(self.local_worker_ids)
+
+
+class ShardedFedServer(_ShardedMixin, FedServer):
+    """FedServer whose round is spread over all ranks (one process per GPU)."""
+
+    def __init__(self, group=None, chunks=4, **kwargs):
+        self._init_shard(kwargs["worker_number"], group, chunks)
+        super().__init__(**kwargs)
+
+    def get_subset_model(self, client_subset):
+        if not client_subset:
+            return self.prev_model
+        ids = [i for i in client_subset if i in self.parameters]
+        ns = [self.parameters.n_of(i) for i in ids]
+        total = global_sample_count(ns, self.device, self.group)
+        store = self.parameters.store
+        rows = [self.parameters.row_of(i) for i in ids]
+        out = torch.zeros(store.layout.P, dtype=torch.float32, device=self.device)
+        if rows:
+            self._aggregate(store, rows, ns, total=total, out=out)
+        allreduce_chunked(out, self.chunks, self.group)
+        return store.layout.views(out)
+
+    def _aggregate(self, store, rows, ns, total=None, out=None):
+        if out is None:
+            return super()._aggregate(store, rows, ns, total)
+        from .servers.fed_server import _MODES
+        return store.fedavg(rows, ns, mode=_MODES[self.aggregation_mode], total=total, out=out)
+
+
+class ShardedFedQuantServer(_ShardedMixin, FedQuantServer):
+    def __init__(self, group=None, chunks=4, **kwargs):
+        self._init_shard(kwargs["worker_number"], group, chunks)
+        super().__init__(**kwargs)
+
+    def get_subset_model(self, client_subset):
+        if not client_subset:
+            return self.prev_model
+        ids = [i for i in client_subset if i in self.parameters]
+        ns = [self.parameters.n_of(i) for i in ids]
+        total = global_sample_count(ns, self.device, self.group)
+        store = self.parameters.store
+        out = torch.zeros(store.layout.P, dtype=torch.float32, device=self.device)
+        if ids:
+            store.fedavg([self.parameters.row_of(i) for i in ids], ns, out=out, total=total)
+        allreduce_chunked(out, self.chunks, self.group)
+        return store.layout.views(out)
+
+
+class ShardedSignSGDServer(SignSGDServer):
+    """Vote over clients on all ranks: local int32 counts, SUM all-reduce, sign."""
+
+    def __init__(self, group=None, **kwargs):
+        super().__init__(**kwargs)
+        self.group = group
+        world, rank = _world()
+        self.local_worker_ids = local_workers(self.worker_number, rank, world)
+
+    def _process_worker_data(self, sign_gradient, __=None):
+        slot = len(self.sign_gradients)
+        if self._planes is not None and slot >= self._planes.shape[0]:
+            raise RuntimeError("more sign gradients than local workers")
+        self._store_client(slot, sign_gradient)
+        self.sign_gradients.append(slot)
+        if len(self.sign_gradients) != len(self.local_worker_ids):
+            return None
+        bad = int(self._bad.item())
+        if bad:
+            self._bad.zero_()
+            self.sign_gradients = []
+            raise ValueError(f"sign gradients hold {bad} values outside {{-1, 0, +1}}")
+        P = self._layout.P
+        counts = torch.empty(P, dtype=torch.int32, device=self.device)
+        self._count(len(self.sign_gradients), P, counts)
+        if _world()[0] > 1:
+            dist.all_reduce(counts, group=self.group)
+        sign_out = torch.empty(P, dtype=torch.float32, device=self.device)
+        vote_planes = torch.empty(_native.sign_words(P), dtype=torch.int64, device=self.device)
+        self._from_counts(counts, P, sign_out, vote_planes)
+        result = SignVoteResult(self._layout.views(sign_out).values())
+        result.vote_planes = vote_planes
+        result.counts = counts
+        self.sign_gradients = []
+        return RepeatedResult(data=result, num=len(self.local_worker_ids))
+
+    def _count(self, K, P, counts):
+        _native.sign_vote_count(self._planes, None, K, P, counts)
+
+    def _from_counts(self, counts, P, sign_out, vote_planes):
+        _native.sign_from_counts(counts, P, sign_out, vote_planes)
+
+    def _ensure(self, shapes):
+        first = self._layout is None
+        super()._ensure(shapes)
+        if first and self._planes.shape[0] != len(self.local_worker_ids):
+            self._planes = self._planes[: max(1, len(self.local_worker_ids))].contiguous()

@@ -160,10 +160,11 @@ class QuantizedClientStore:
                 self.F[row, ql.src[i]:ql.src[i] + n].copy_(v.reshape(-1).float(),
                                                            non_blocking=True)
 
-    def fedavg(self, rows, ns, out=None):
+    def fedavg(self, rows, ns, out=None, total=None):
         if out is None:
             out = torch.empty(self.layout.P, dtype=torch.float32, device=self.device)
-        total = sum(int(n) for n in ns)
+        if total is None:
+            total = sum(int(n) for n in ns)
         rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
         w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
         _native.dequant_fedavg(self.tiles, self.ntiles, self.Q, self.F, self.sz, rows_t, w_t,

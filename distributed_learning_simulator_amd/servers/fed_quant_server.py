@@ -48,8 +48,8 @@ class FedQuantServer(FedServer):
         # aggregation kernel (see module docstring).
         return client_parameter
 
-    def _aggregate(self, store, rows, ns):
-        return store.fedavg(rows, ns)
+    def _aggregate(self, store, rows, ns, total=None):
+        return store.fedavg(rows, ns, total=total)
 
     def _process_aggregated_parameter(self, aggregated_parameter: dict):
         log.info("begin quantization")

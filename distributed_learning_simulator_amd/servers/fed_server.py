@@ -29,7 +29,13 @@ class FedServer(Server):
         self.__prev_model = copy.deepcopy(
             ModelUtil(self.tester.model).get_parameter_dict()) if self.tester is not None else {}
         self.worker_data_queue.put_result(
-            RepeatedResult(data=self.prev_model, num=self.worker_number))
+            RepeatedResult(data=self.prev_model, num=self.clients_per_round))
+
+    @property
+    def clients_per_round(self):
+        """Clients whose updates this process receives per round (all of them here;
+        the sharded servers in ``distributed.py`` override it)."""
+        return self.worker_number
 
     def _make_store(self, parameter_dict):
         return ClientUpdateStore(ParameterLayout.from_dict(parameter_dict), self.device,
@@ -68,8 +74,8 @@ class FedServer(Server):
                                [self.parameters.n_of(i) for i in ids])
         return store.layout.views(flat)
 
-    def _aggregate(self, store, rows, ns):
-        return store.fedavg(rows, ns, mode=_MODES[self.aggregation_mode])
+    def _aggregate(self, store, rows, ns, total=None):
+        return store.fedavg(rows, ns, mode=_MODES[self.aggregation_mode], total=total)
 
     def _process_worker_data(self, data, __):
         worker_id, training_dataset_size, parameter_dict = data
@@ -77,8 +83,8 @@ class FedServer(Server):
             training_dataset_size,
             self._process_client_parameter(parameter_dict),
         )
-        if len(self.parameters) != self.worker_number:
-            log.debug("%s %s,skip", len(self.parameters), self.worker_number)
+        if len(self.parameters) != self.clients_per_round:
+            log.debug("%s %s,skip", len(self.parameters), self.clients_per_round)
             return None
         self.round += 1
         log.info("begin aggregating")

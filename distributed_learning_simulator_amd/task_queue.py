@@ -15,12 +15,26 @@ import torch
 
 
 class RepeatedResult:
+    """A result handed to ``num`` distinct consumers (servers/fed_server.py:88-91)."""
+
     def __init__(self, data, num):
         self.data = data
         self.num = num
+        self.consumers = set()
 
 
 _STOP = object()
+_consumer = threading.local()  # a fresh token per thread (thread idents are reused)
+_consumer_ids = iter(range(1 << 62))
+_consumer_lock = threading.Lock()
+
+
+def _thread_token():
+    tok = getattr(_consumer, "token", None)
+    if tok is None:
+        with _consumer_lock:
+            tok = _consumer.token = ("thread", next(_consumer_ids))
+    return tok
 
 
 class ThreadTaskQueue:
@@ -64,21 +78,38 @@ class ThreadTaskQueue:
             self._results.append(result)
             self._cv.notify_all()
 
-    def get_result(self, timeout=None):
+    def get_result(self, timeout=None, consumer=None):
+        """Next result this consumer (default: the calling thread) has not taken yet.
+
+        A fast worker that asks for round r+1 while slower workers still hold
+        round r's broadcast must not take round r's copy twice, so a
+        RepeatedResult is served once per consumer and retired after ``num``."""
+        key = _thread_token() if consumer is None else consumer
+
+        def pick():
+            for i, r in enumerate(self._results):
+                if isinstance(r, RepeatedResult):
+                    if key not in r.consumers:
+                        return i
+                else:
+                    return i
+            return None
+
         with self._cv:
-            ok = self._cv.wait_for(lambda: self._results or self._error is not None, timeout)
+            ok = self._cv.wait_for(lambda: pick() is not None or self._error is not None, timeout)
             if self._error is not None:
                 raise RuntimeError("server queue task failed") from self._error
             if not ok:
                 raise TimeoutError("ThreadTaskQueue.get_result timed out")
-            head = self._results[0]
-            if isinstance(head, RepeatedResult):
-                head.num -= 1
-                if head.num <= 0:
-                    self._results.popleft()
-                return head.data
-            self._results.popleft()
-            return head
+            i = pick()
+            r = self._results[i]
+            if isinstance(r, RepeatedResult):
+                r.consumers.add(key)
+                if len(r.consumers) >= r.num:
+                    del self._results[i]
+                return r.data
+            del self._results[i]
+            return r
 
     def stop(self):
         self.add_task(_STOP)

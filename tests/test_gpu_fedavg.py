@@ -155,8 +155,8 @@ def test_fed_server_round_golden():
     for wid in order:
         d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
         server.worker_data_queue.add_task((int(wid), int(n[wid]), d))
-    for _ in range(case["K"]):  # the initial broadcast of the previous model, once per worker
-        server.worker_data_queue.get_result()
-    res = server.worker_data_queue.get_result()
+    for w in range(case["K"]):  # the initial broadcast of the previous model, once per worker
+        server.worker_data_queue.get_result(consumer=w)
+    res = server.worker_data_queue.get_result(consumer=0)
     flat = np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout])
     assert same_bits(flat, z[f"{k}_full"])

@@ -63,11 +63,11 @@ def test_fed_quant_server_round_golden():
     server = FedQuantServer(tester=None, worker_number=K, synchronous=True)
     for i, p in enumerate(payloads):
         server.worker_data_queue.add_task((i, int(z["n"][i]), p))
-    for _ in range(K):
-        server.worker_data_queue.get_result()
+    for w in range(K):
+        server.worker_data_queue.get_result(consumer=w)
     assert same_bits(flat(server.last_aggregate, case["layout"]), z["agg"])
     # the broadcast model is the re-quantized aggregate (this build's contract, D4)
-    res = server.worker_data_queue.get_result()
+    res = server.worker_data_queue.get_result(consumer=0)
     agg = z["agg"]
     q, sc, zp, deq = oquant.requantize_tensors(agg, case["layout"])
     assert same_bits(flat(res, case["layout"]), deq)

@@ -49,8 +49,8 @@ def _run_round(server, case, layout, U):
     for i in range(K):
         d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[i], layout).items()}
         server.worker_data_queue.add_task((i, int(case["n"][i]), d))
-    for _ in range(2 * K):  # initial broadcast + this round's broadcast
-        server.worker_data_queue.get_result()
+    for w in range(2 * K):  # initial broadcast + this round's broadcast
+        server.worker_data_queue.get_result(consumer=w % K)
     return server.shapley_values[1]
 
 
