@@ -285,6 +285,57 @@ def bench_shapley_gemm(args, dev):
     }
 
 
+def bench_shapley_evals(args, dev):
+    """Config 5b: Shapley utility evaluations — subset model (reference-order
+    kernel) + CIFAR-10-shaped test-set inference of ResNet-18 (fp32)."""
+    from distributed_learning_simulator_amd.layout import ParameterLayout as PL
+    from distributed_learning_simulator_amd.model_util import ModelUtil
+    from distributed_learning_simulator_amd.models import ResNet18
+    torch.manual_seed(SEED + 6)
+    teacher = ResNet18().to(dev).eval()
+    X = torch.randn(args.eval_images, 3, 32, 32, device=dev)
+    with torch.no_grad():
+        y = torch.cat([teacher(X[i:i + 1000]).argmax(1) for i in range(0, X.shape[0], 1000)])
+    base = ModelUtil(teacher).get_parameter_dict()
+    layout = PL.from_dict(base)
+    K = 50
+    row = layout.flatten(base, device=dev)
+    U = row[None, :].repeat(K, 1)
+    U.add_(torch.randn_like(U) * 0.002)
+    n = [100 + 17 * i for i in range(K)]
+    g = torch.Generator().manual_seed(SEED + 6)
+    coalitions = [sorted(torch.randperm(K, generator=g)[: 1 + i % K].tolist())
+                  for i in range(args.evals + 2)]
+    model = ResNet18().to(dev).eval()
+    mu = ModelUtil(model)
+
+    def one_eval(c):
+        rows = torch.tensor(c, dtype=torch.int32, device=dev)
+        w = torch.tensor([n[i] for i in c], dtype=torch.float32, device=dev)
+        out = torch.empty(layout.P, device=dev)
+        _native.fedavg(U, rows, w, float(sum(n[i] for i in c)), layout.P, out)
+        mu.load_parameter_dict(layout.views(out))
+        correct = 0
+        with torch.no_grad():
+            for i in range(0, X.shape[0], 2500):
+                correct += int((model(X[i:i + 2500]).argmax(1) == y[i:i + 2500]).sum())
+        return correct / X.shape[0]
+
+    for c in coalitions[:2]:
+        one_eval(c)  # MIOpen kernel selection
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    accs = [one_eval(c) for c in coalitions[2:]]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    del U
+    return {"config": f"Shapley utility evals: subset model + ResNet-18 inference on "
+                      f"{args.eval_images} CIFAR-10-shaped images (fp32), 50 clients",
+            "value": round(len(accs) / el, 3), "unit": "subset-evals/s per GPU",
+            "ms_per_eval": round(el / len(accs) * 1e3, 2),
+            "utility_range": [round(min(accs), 4), round(max(accs), 4)]}
+
+
 # ---------------------------------------------------------- CPU baseline
 def cpu_baseline(args):
     """Reference torch op sequence (servers/fed_server.py:52-65) on the host CPU."""
@@ -329,6 +380,8 @@ def main():
     ap.add_argument("--clients", type=int, default=100, help="client updates per GPU")
     ap.add_argument("--chunks", type=int, default=4, help="all-reduce pipeline chunks (N>1)")
     ap.add_argument("--subsets", type=int, default=50)
+    ap.add_argument("--evals", type=int, default=8, help="timed Shapley utility evaluations")
+    ap.add_argument("--eval-images", type=int, default=10000)
     ap.add_argument("--quick", action="store_true", help="headline only (no components)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-clients", type=int, default=20)
@@ -348,7 +401,8 @@ def main():
     components = {}
     if not args.quick and rank == 0:
         for name, fn in (("sign_vote", bench_sign), ("fed_quant", bench_quant),
-                         ("shapley_gemm", bench_shapley_gemm)):
+                         ("shapley_gemm", bench_shapley_gemm),
+                         ("shapley_evals", bench_shapley_evals)):
             try:
                 components[name] = fn(args, dev)
                 log(name, json.dumps(components[name]))

@@ -50,10 +50,27 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
     const int lane = __lane_id();
     const int h = lane >> 5, col = lane & 31;
     const int wave = threadIdx.x >> 6;
-    for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles;
-         tile += (int64_t)gridDim.x * kWaves) {
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
+    if (tile >= ntiles) return;
+    const int nsteps = Kp / 2;  // multiple of 4 (Kp padded to 8)
+
+    // One flattened (tile, k-step) stream: the U loads of the next 4 k-steps are
+    // in flight while the MFMAs of the current one run, and across a tile seam
+    // they already fetch the next tile, so the epilogue stores overlap them.
+    auto loadB = [&](int64_t t, int s) -> f32x4 {
+        const int64_t pp = t * kTileP + 4 * col;
+        const int32_t r = srow[2 * s + h];
+        f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (r >= 0 && t < ntiles && pp + 4 <= P)
+            b = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + pp));
+        return b;
+    };
+    f32x4 b0 = loadB(tile, 0), b1 = loadB(tile, 1), b2 = loadB(tile, 2), b3 = loadB(tile, 3);
+    for (; tile < ntiles; tile += stride) {
         const int64_t p = tile * kTileP + 4 * col;  // this lane's 4 parameters
         const bool inb = p + 4 <= P;
+        const int64_t next = tile + stride;
         f32x16 acc[MT][4];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -71,16 +88,6 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                 }
             }
         }
-        // software pipeline: the U loads of the next 4 k-steps are in flight while
-        // the MFMAs of the current one run (named registers, no runtime indexing)
-        auto loadB = [&](int s) -> f32x4 {
-            const int32_t r = srow[2 * s + h];
-            f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (r >= 0 && inb)
-                b = __builtin_nontemporal_load(
-                    reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + p));
-            return b;
-        };
         auto mma = [&](int s, const f32x4 &b) {
             const int k = 2 * s + h;
 #pragma unroll
@@ -91,17 +98,18 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                     acc[mt][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[n], acc[mt][n], 0, 0, 0);
             }
         };
-        const int nsteps = Kp / 2;  // multiple of 4 (Kp padded to 8)
-        f32x4 b0 = loadB(0), b1 = loadB(1), b2 = loadB(2), b3 = loadB(3);
         for (int s = 0; s < nsteps; s += 4) {
+            const bool seam = s + 4 >= nsteps;
+            const int64_t lt = seam ? next : tile;
+            const int ls = seam ? s + 4 - nsteps : s + 4;
             mma(s, b0);
-            b0 = loadB(s + 4);
+            b0 = loadB(lt, ls);
             mma(s + 1, b1);
-            b1 = loadB(s + 5);
+            b1 = loadB(lt, ls + 1);
             mma(s + 2, b2);
-            b2 = loadB(s + 6);
+            b2 = loadB(lt, ls + 2);
             mma(s + 3, b3);
-            b3 = loadB(s + 7);
+            b3 = loadB(lt, ls + 3);
         }
         if (inb) {
 #pragma unroll
@@ -116,6 +124,21 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
             }
         }
     }
+}
+
+template <int MT, bool BETA>
+unsigned grid_blocks(int64_t ntiles, size_t lds) {
+    // exactly the resident blocks (persistent): every wave gets ntiles/(blocks*4) tiles
+    int slot = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&slot, k_subset_gemm<MT, BETA>, kBlock, lds) !=
+            hipSuccess || slot < 1)
+        slot = 1;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t want = (ntiles + kWaves - 1) / kWaves;
+    const int64_t cap = (int64_t)slot * cus;
+    return (unsigned)(want < cap ? want : cap);
 }
 
 }  // namespace
@@ -133,8 +156,6 @@ extern "C" int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const f
                 DLS_ELAYOUT, "dls_subset_gemm_f32: P, ldu, ldo multiples of 4; 16-byte alignment");
     hipStream_t st = as_stream(stream);
     const int64_t ntiles = (P + kTileP - 1) / kTileP;
-    const int64_t want = (ntiles + kWaves - 1) / kWaves;
-    const unsigned blocks = (unsigned)(want < 2048 ? want : 2048);
     // S in chunks of 64 subsets (two 32-row MFMA tiles), K in chunks of 256 clients
     for (int s0 = 0; s0 < S; s0 += 64) {
         const int Sc = S - s0 < 64 ? S - s0 : 64;
@@ -148,8 +169,9 @@ extern "C" int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const f
             const int beta = k0 > 0;
             float *oc = out + (int64_t)s0 * ldo;
 #define DLS_GEMM_LAUNCH(MT_, B_)                                                              \
-    hipLaunchKernelGGL((k_subset_gemm<MT_, B_>), dim3(blocks), dim3(kBlock), lds, st, Cc,      \
-                       (int64_t)K, Sc, Kc, U, ldu, rows + k0, P, oc, ldo, ntiles)
+    hipLaunchKernelGGL((k_subset_gemm<MT_, B_>), dim3(grid_blocks<MT_, B_>(ntiles, lds)),      \
+                       dim3(kBlock), lds, st, Cc, (int64_t)K, Sc, Kc, U, ldu, rows + k0, P, oc,  \
+                       ldo, ntiles)
             if (MT == 2 && beta) DLS_GEMM_LAUNCH(2, true);
             else if (MT == 2) DLS_GEMM_LAUNCH(2, false);
             else if (beta) DLS_GEMM_LAUNCH(1, true);

@@ -131,13 +131,17 @@ struct HSCounter {
 // One lane owns one group of 64 parameters (one 16-byte [pos, neg] load per
 // client, 16 clients in flight).  Outputs: counts (int32, optional) and/or
 // fp32 signs.  Exact: the counters hold K < 16 * 2^CB.
+// 64-thread blocks: one wave per block, so ~P/64/64 waves spread evenly over
+// the 256 CUs (256-thread blocks left 3-vs-2 blocks per CU, a 12% tail).
+constexpr int kVoteBlock = 64;
+
 template <int CB>
-__global__ __launch_bounds__(kBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
+__global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
                                                       int64_t ldp, const int32_t *__restrict__ rows,
                                                       int K, int64_t P, int64_t ngroups,
                                                       int32_t *__restrict__ counts,
                                                       float *__restrict__ sign_out) {
-    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t g = (int64_t)blockIdx.x * kVoteBlock + threadIdx.x;
     if (g >= ngroups) return;
     HSCounter<CB> cp, cn;
     uint64_t nan = 0;
@@ -314,8 +318,8 @@ template <int CB>
 int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K, int64_t P,
                 int32_t *counts, float *sign_out, hipStream_t st) {
     const int64_t ngroups = (P + 63) / 64;
-    const dim3 grid((unsigned)((ngroups + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL((k_sign_vote<CB>), grid, dim3(kBlock), 0, st, planes, ldp, rows, K, P,
+    const dim3 grid((unsigned)((ngroups + kVoteBlock - 1) / kVoteBlock));
+    hipLaunchKernelGGL((k_sign_vote<CB>), grid, dim3(kVoteBlock), 0, st, planes, ldp, rows, K, P,
                        ngroups, counts, sign_out);
     return check_launch("dls_sign_vote");
 }

@@ -14,3 +14,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
         python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.log" || exit $?
 done
 echo "profiles in $OUT"
+# SQ instruction / stall counters (one pass: 8 SQ + GRBM)
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_SQ" -o run -- \
+    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --evals 1 > "$OUT/pmc_SQ.json" 2> "$OUT/pmc_SQ.log" || exit $?
+echo "sq counters done"
