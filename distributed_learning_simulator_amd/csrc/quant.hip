@@ -65,7 +65,7 @@ __device__ __forceinline__ void int_chunk_loop(float (&acc)[16], const uint8_t *
                                                int64_t ldc, const int32_t *__restrict__ rows,
                                                const float *__restrict__ w, int K, int split,
                                                const FastDiv &d) {
-    constexpr int U = 4;  // clients in flight per lane
+    constexpr int U = 3;  // clients per batch (two batches in flight per lane)
     const f32x2 zero2 = f32x2{0.f, 0.f};
     {
         const int64_t row = rows[0];
@@ -74,19 +74,39 @@ __device__ __forceinline__ void int_chunk_loop(float (&acc)[16], const uint8_t *
         const f32x2 b = TWO ? szc[row * ldc + 1] : zero2;
         accum16<SIGNED, TWO, true>(acc, qv, a, b, w[0], split, d);
     }
-    int k = 1;
-    for (; k + U <= K; k += U) {
+    // batches of U clients, double-buffered: batch b+1 loads while batch b computes
+    struct Batch {
         u32x4 qv[U];
         f32x2 a[U], b[U];
+    };
+    auto load = [&](int k0, Batch &bt) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t row = rows[k + u];
-            qv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
-            a[u] = szc[row * ldc];
-            b[u] = TWO ? szc[row * ldc + 1] : zero2;
+            const int64_t row = rows[k0 + u];
+            bt.qv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
+            bt.a[u] = szc[row * ldc];
+            bt.b[u] = TWO ? szc[row * ldc + 1] : zero2;
         }
+    };
+    auto consume = [&](int k0, const Batch &bt) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) accum16<SIGNED, TWO, false>(acc, qv[u], a[u], b[u], w[k + u], split, d);
+        for (int u = 0; u < U; ++u)
+            accum16<SIGNED, TWO, false>(acc, bt.qv[u], bt.a[u], bt.b[u], w[k0 + u], split, d);
+    };
+    int k = 1;
+    const int nfull = (K - 1) / U;  // full batches after the peeled first client
+    if (nfull > 0) {
+        Batch A, B;
+        load(k, A);
+        for (int bi = 0; bi < nfull; bi += 2) {
+            if (bi + 1 < nfull) load(k + U, B);
+            consume(k, A);
+            k += U;
+            if (bi + 1 >= nfull) break;
+            if (bi + 2 < nfull) load(k + U, A);
+            consume(k, B);
+            k += U;
+        }
     }
     for (; k < K; ++k) {
         const int64_t row = rows[k];

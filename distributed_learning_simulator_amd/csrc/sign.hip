@@ -7,7 +7,7 @@
 // Vote (servers/sign_sgd_server.py:12-21): counts = #pos - #neg per parameter,
 // accumulated with bit-sliced ("vertical") counters: one 64-bit word per
 // counter bit holds that bit of 64 parameters' counts, fed by a carry-save
-// (Harley-Seal) adder tree, so 16 clients cost 15 CSAs (5 bitwise ops each)
+// (Harley-Seal) adder tree, so 8 clients cost 7 CSAs (5 bitwise ops each)
 // per plane word and no per-parameter unpacking; the counters are unpacked
 // once at the end.  Exact in any order.
 #include "dls_common.h"
@@ -54,33 +54,41 @@ __device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *
     if (lane < valid_words) dst_tile[lane] = w;  // a tensor's last tile may end early
 }
 
-// grid: x = tile blocks (4 tiles per block), y = client.
+// grid: x = blocks of 4 waves x kPackTPW tiles, y = client.  Each wave issues
+// the loads of its kPackTPW tiles before packing any (memory-level parallelism).
+constexpr int kPackTPW = 4;
+
 __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ X, int64_t ldx,
                                                       int64_t P, uint64_t *__restrict__ planes,
                                                       int64_t ldp, int64_t ntiles,
                                                       int32_t *nonternary) {
-    const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (tile >= ntiles) return;  // wave-uniform
+    const int64_t t0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kPackTPW;
+    if (t0 >= ntiles) return;  // wave-uniform
     const int64_t k = blockIdx.y;
     const int lane = __lane_id();
-    const int64_t e = tile * 256 + 4 * lane;
     const float *row = X + k * ldx;
-    f32x4 v;
-    if (e + 4 <= P) {
-        v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(row + e));
-    } else {
-        v = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int c = 0; c < 4; ++c)
-            if (e + c < P) v[c] = row[e + c];
+    f32x4 v[kPackTPW];
+#pragma unroll
+    for (int i = 0; i < kPackTPW; ++i) {
+        const int64_t e = (t0 + i) * 256 + 4 * lane;
+        if (e + 4 <= P) {
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(row + e));
+        } else {
+            v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int c = 0; c < 4; ++c)
+                if (e + c < P) v[i][c] = row[e + c];
+        }
     }
-    pack_tile(v, planes + k * ldp + tile * 8, nonternary);
+#pragma unroll
+    for (int i = 0; i < kPackTPW; ++i)
+        if (t0 + i < ntiles) pack_tile(v[i], planes + k * ldp + (t0 + i) * 8, nonternary);
 }
 
 // ---------------------------------------------------------------- vote
-// Carry-save (Harley-Seal) accumulation of 16 one-bit planes: ones/twos/fours/
-// eights are carry-save partial counts, every 16 inputs emit a "sixteens" word
-// that ripples into the CB-bit counter c (in units of 16).  15 CSAs of 5 ops
-// per 16 clients instead of 16 ripple increments of 2*B ops.
+// Carry-save (Harley-Seal) accumulation of 8 one-bit planes: ones/twos/fours
+// are carry-save partial counts, every 8 inputs emit an "eights" word that
+// ripples into the CB-bit counter c (in units of 8).  7 CSAs of 5 ops per 8
+// clients instead of 8 ripple increments of 2*B ops.
 __device__ __forceinline__ void csa(uint64_t &h, uint64_t &l, uint64_t a, uint64_t b, uint64_t c) {
     const uint64_t u = a ^ b;
     h = (a & b) | (u & c);
@@ -89,48 +97,41 @@ __device__ __forceinline__ void csa(uint64_t &h, uint64_t &l, uint64_t a, uint64
 
 template <int CB>
 struct HSCounter {
-    uint64_t ones = 0, twos = 0, fours = 0, eights = 0;
+    // carry-save partial counts (ones/twos/fours) + CB-bit counter of eights
+    uint64_t ones = 0, twos = 0, fours = 0;
     uint64_t c[CB];
     __device__ __forceinline__ HSCounter() {
 #pragma unroll
         for (int b = 0; b < CB; ++b) c[b] = 0;
     }
-    __device__ __forceinline__ void add16(const uint64_t (&x)[16]) {
-        uint64_t twosA, twosB, foursA, foursB, eightsA, eightsB, sixteens;
+    __device__ __forceinline__ void add8(const uint64_t (&x)[8]) {
+        uint64_t twosA, twosB, foursA, foursB, eights;
         csa(twosA, ones, ones, x[0], x[1]);
         csa(twosB, ones, ones, x[2], x[3]);
         csa(foursA, twos, twos, twosA, twosB);
         csa(twosA, ones, ones, x[4], x[5]);
         csa(twosB, ones, ones, x[6], x[7]);
         csa(foursB, twos, twos, twosA, twosB);
-        csa(eightsA, fours, fours, foursA, foursB);
-        csa(twosA, ones, ones, x[8], x[9]);
-        csa(twosB, ones, ones, x[10], x[11]);
-        csa(foursA, twos, twos, twosA, twosB);
-        csa(twosA, ones, ones, x[12], x[13]);
-        csa(twosB, ones, ones, x[14], x[15]);
-        csa(foursB, twos, twos, twosA, twosB);
-        csa(eightsB, fours, fours, foursA, foursB);
-        csa(sixteens, eights, eights, eightsA, eightsB);
+        csa(eights, fours, fours, foursA, foursB);
 #pragma unroll
-        for (int b = 0; b < CB; ++b) {  // c += sixteens (bit-sliced ripple)
-            const uint64_t t = c[b] & sixteens;
-            c[b] ^= sixteens;
-            sixteens = t;
+        for (int b = 0; b < CB; ++b) {  // c += eights (bit-sliced ripple)
+            const uint64_t t = c[b] & eights;
+            c[b] ^= eights;
+            eights = t;
         }
     }
     __device__ __forceinline__ int count(int j) const {
         int v = (int)((ones >> j) & 1u) | ((int)((twos >> j) & 1u) << 1) |
-                ((int)((fours >> j) & 1u) << 2) | ((int)((eights >> j) & 1u) << 3);
+                ((int)((fours >> j) & 1u) << 2);
 #pragma unroll
-        for (int b = 0; b < CB; ++b) v |= (int)((c[b] >> j) & 1u) << (4 + b);
+        for (int b = 0; b < CB; ++b) v |= (int)((c[b] >> j) & 1u) << (3 + b);
         return v;
     }
 };
 
 // One lane owns one group of 64 parameters (one 16-byte [pos, neg] load per
-// client, 16 clients in flight).  Outputs: counts (int32, optional) and/or
-// fp32 signs.  Exact: the counters hold K < 16 * 2^CB.
+// client, two batches of 8 clients in flight).  Outputs: counts (int32, optional) and/or
+// fp32 signs.  Exact: the counters hold K < 8 * 2^CB.
 // 64-thread blocks: one wave per block, so ~P/64/64 waves spread evenly over
 // the 256 CUs (256-thread blocks left 3-vs-2 blocks per CU, a 12% tail).
 constexpr int kVoteBlock = 64;
@@ -147,36 +148,47 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
     uint64_t nan = 0;
     const u64x2 *base = reinterpret_cast<const u64x2 *>(planes) + g;
     const int64_t ldp2 = ldp / 2;
-    for (int j = 0; j < K; j += 16) {
-        uint64_t xp[16], xn[16];
-        if (j + 16 <= K) {
-            u64x2 w[16];
+    // Batches of 8 clients, double-buffered: batch b+1's 8 loads are in flight
+    // while batch b runs through the carry-save adders (the vote is latency-bound
+    // at a few waves per SIMD otherwise).
+    constexpr int B8 = 8;
+    auto load8 = [&](int j, u64x2 (&w)[B8]) {
+        if (j + B8 <= K) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
+            for (int u = 0; u < B8; ++u) {
                 const int64_t r = rows ? rows[j + u] : (j + u);
                 w[u] = __builtin_nontemporal_load(base + r * ldp2);
             }
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                xp[u] = w[u][0];
-                xn[u] = w[u][1];
-            }
         } else {  // tail: missing clients count as zero planes
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                xp[u] = xn[u] = 0;
+            for (int u = 0; u < B8; ++u) {
+                w[u] = u64x2{0, 0};
                 if (j + u < K) {
                     const int64_t r = rows ? rows[j + u] : (j + u);
-                    const u64x2 w = base[r * ldp2];
-                    xp[u] = w[0];
-                    xn[u] = w[1];
+                    w[u] = base[r * ldp2];
                 }
             }
         }
+    };
+    auto consume8 = [&](const u64x2 (&w)[B8]) {
+        uint64_t xp[B8], xn[B8];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) nan |= xp[u] & xn[u];
-        cp.add16(xp);
-        cn.add16(xn);
+        for (int u = 0; u < B8; ++u) {
+            xp[u] = w[u][0];
+            xn[u] = w[u][1];
+            nan |= xp[u] & xn[u];
+        }
+        cp.add8(xp);
+        cn.add8(xn);
+    };
+    u64x2 wa[B8], wb[B8];
+    load8(0, wa);
+    for (int j = 0; j < K; j += 2 * B8) {
+        if (j + B8 < K) load8(j + B8, wb);
+        consume8(wa);
+        if (j + B8 >= K) break;
+        if (j + 2 * B8 < K) load8(j + 2 * B8, wa);
+        consume8(wb);
     }
     const int64_t e0 = g * 64;
     const bool full = e0 + 64 <= P;
@@ -326,8 +338,8 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
 
 int vote_dispatch(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K, int64_t P,
                   int32_t *counts, float *sign_out, hipStream_t st) {
-    // counts reach 16*c + 15 with c <= ceil(K/16) < 2^CB (fewer bits = fewer ops/registers)
-    const int64_t c_max = (K + 15) / 16;
+    // counts reach 8*c + 7 with c <= ceil(K/8) < 2^CB (fewer bits = fewer ops/registers)
+    const int64_t c_max = (K + 7) / 8;
     if (c_max < (1 << 2)) return launch_vote<2>(planes, ldp, rows, K, P, counts, sign_out, st);
     if (c_max < (1 << 4)) return launch_vote<4>(planes, ldp, rows, K, P, counts, sign_out, st);
     if (c_max < (1 << 6)) return launch_vote<6>(planes, ldp, rows, K, P, counts, sign_out, st);
@@ -353,7 +365,8 @@ extern "C" int dls_sign_pack_f32(const float *X, int64_t ldx, int32_t K, int64_t
                 "dls_sign_pack_f32: ldx=%lld (multiple of 4, >= P) ldp=%lld (>= %lld)",
                 (long long)ldx, (long long)ldp, (long long)DLS_SIGN_WORDS(P));
     const int64_t ntiles = (P + 255) / 256;
-    const dim3 grid((unsigned)((ntiles + 3) / 4), (unsigned)K);
+    const int64_t per_block = (kBlock / 64) * kPackTPW;
+    const dim3 grid((unsigned)((ntiles + per_block - 1) / per_block), (unsigned)K);
     hipLaunchKernelGGL(k_sign_pack, grid, dim3(kBlock), 0, as_stream(stream), X, ldx, P, planes,
                        ldp, ntiles, nonternary);
     return check_launch("dls_sign_pack_f32");
