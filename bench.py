@@ -308,6 +308,7 @@ def bench_shapley_evals(args, dev):
                   for i in range(args.evals + 2)]
     model = ResNet18().to(dev).eval()
     mu = ModelUtil(model)
+    autocast = {"enabled": False}
 
     def one_eval(c):
         rows = torch.tensor(c, dtype=torch.int32, device=dev)
@@ -316,24 +317,34 @@ def bench_shapley_evals(args, dev):
         _native.fedavg(U, rows, w, float(sum(n[i] for i in c)), layout.P, out)
         mu.load_parameter_dict(layout.views(out))
         correct = 0
-        with torch.no_grad():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16,
+                                             enabled=autocast["enabled"]):
             for i in range(0, X.shape[0], 2500):
                 correct += int((model(X[i:i + 2500]).argmax(1) == y[i:i + 2500]).sum())
         return correct / X.shape[0]
 
-    for c in coalitions[:2]:
-        one_eval(c)  # MIOpen kernel selection
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    accs = [one_eval(c) for c in coalitions[2:]]
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    def timed():
+        for c in coalitions[:2]:
+            one_eval(c)  # MIOpen kernel selection
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        accs = [one_eval(c) for c in coalitions[2:]]
+        torch.cuda.synchronize()
+        return accs, time.perf_counter() - t0
+
+    accs, el = timed()
+    autocast["enabled"] = True
+    model.to(memory_format=torch.channels_last)
+    X = X.to(memory_format=torch.channels_last)
+    accs16, el16 = timed()
     del U
     return {"config": f"Shapley utility evals: subset model + ResNet-18 inference on "
                       f"{args.eval_images} CIFAR-10-shaped images (fp32), 50 clients",
             "value": round(len(accs) / el, 3), "unit": "subset-evals/s per GPU",
             "ms_per_eval": round(el / len(accs) * 1e3, 2),
-            "utility_range": [round(min(accs), 4), round(max(accs), 4)]}
+            "utility_range": [round(min(accs), 4), round(max(accs), 4)],
+            "bf16_autocast_value": round(len(accs16) / el16, 3),
+            "bf16_max_utility_diff": round(max(abs(a - b) for a, b in zip(accs, accs16)), 4)}
 
 
 # ---------------------------------------------------------- CPU baseline
