@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace --stats run: per-kernel calls / avg / min / max.
+
+    python tools/trace_summary.py gpurun_out/prof_r01/trace/run_kernel_stats.csv > profiles/r01_kernel_stats.txt
+"""
+import csv
+import re
+import sys
+
+
+def short(name):
+    m = re.search(r"(k_\w+(<[^>]*>)?)", name)
+    return m.group(1) if m else name[:60]
+
+
+def main(path):
+    rows = list(csv.DictReader(open(path)))
+    print(f"# rocprofv3 --kernel-trace --stats summary of {path}")
+    print(f"{'kernel':44s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} {'share%':>7s}")
+    for r in rows:
+        if "dls::" not in r["Name"]:
+            continue
+        print(f"{short(r['Name']):44s} {int(r['Calls']):6d} {float(r['AverageNs']) / 1e3:10.2f} "
+              f"{float(r['MinNs']) / 1e3:10.2f} {float(r['MaxNs']) / 1e3:10.2f} "
+              f"{float(r['Percentage']):7.2f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
