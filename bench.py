@@ -156,6 +156,32 @@ def bench_fedavg(args, dev, rank, world):
 
 
 # ------------------------------------------------------------ components
+def bench_fedavg_k1000(args, dev):
+    """North-star scale: FedAvg of 1000 ResNet-18-sized updates (44.7 GB in HBM)."""
+    layout = ParameterLayout(resnet18_cifar())
+    P, K = layout.P, 1000
+    U, n = synth_updates(K, P, dev, SEED + 7)
+    rows = torch.arange(K, dtype=torch.int32, device=dev)
+    w = torch.tensor(n, dtype=torch.float32, device=dev)
+    out = torch.empty(P, device=dev)
+    total = float(sum(n))
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.fedavg(U, rows, w, total, P, out)
+        if b is not None:
+            b.record()
+
+    wall, kms = timed_launches(step, max(3, args.steps // 4), 2)
+    ms = wall / max(3, args.steps // 4) * 1e3
+    del U
+    return {"config": "FedAvg of 1000 ResNet-18 fp32 updates (44.7 GB), bit-exact reference order",
+            "value": round(K * layout.numel * 4 / (ms / 1e3) / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(ms, 4),
+            "roofline": roofline("dls_fedavg_f32", K * P * 4 + P * 4, kms)}
+
+
 def bench_sign(args, dev):
     layout = ParameterLayout(resnet18_cifar())
     P, K = layout.P, 1000
@@ -395,6 +421,7 @@ def main():
     ap.add_argument("--eval-images", type=int, default=10000)
     ap.add_argument("--quick", action="store_true", help="headline only (no components)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--cpu-clients", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -403,15 +430,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     _native.require_gpu()
+    local = local % torch.cuda.device_count()  # (gloo dry runs may oversubscribe one GPU)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:  # dry runs of the N>1 path on a single-GPU box
+            dist.init_process_group(args.backend)
 
     value, ms, rf, extra = bench_fedavg(args, dev, rank, world)
     components = {}
     if not args.quick and rank == 0:
-        for name, fn in (("sign_vote", bench_sign), ("fed_quant", bench_quant),
+        for name, fn in (("fedavg_k1000", bench_fedavg_k1000), ("sign_vote", bench_sign),
+                         ("fed_quant", bench_quant),
                          ("shapley_gemm", bench_shapley_gemm),
                          ("shapley_evals", bench_shapley_evals)):
             try:

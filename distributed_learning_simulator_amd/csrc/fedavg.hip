@@ -16,6 +16,9 @@ namespace dls {
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef DLS_FEDAVG_UNROLL
+#define DLS_FEDAVG_UNROLL 8
+#endif
 
 template <bool NT>
 __device__ __forceinline__ f32x4 load4(const f32x4 *p) {
@@ -155,7 +158,7 @@ extern "C" int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows,
     hipStream_t st = as_stream(stream);
     if (mode == DLS_FEDAVG_EXACT) {
         const FastDiv d = make_fastdiv(total);
-        hipLaunchKernelGGL((k_fedavg_exact<8, true>), grid, dim3(kBlock), 0, st,
+        hipLaunchKernelGGL((k_fedavg_exact<DLS_FEDAVG_UNROLL, true>), grid, dim3(kBlock), 0, st,
                            reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, d,
                            P4, reinterpret_cast<f32x4 *>(out));
     } else if (mode == DLS_FEDAVG_FMA) {

@@ -14,6 +14,12 @@ namespace dls {
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef DLS_QUANT_U
+#define DLS_QUANT_U 2  // A/B on MI355X: 2 > 3 > 4 clients per batch (tools/ab_bench.py)
+#endif
+#ifndef DLS_QUANT_SCALAR_SZ
+#define DLS_QUANT_SCALAR_SZ 1
+#endif
 
 __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
     return (float)((w >> (8 * k)) & 0xffu);  // selects v_cvt_f32_ubyte{k}
@@ -65,7 +71,7 @@ __device__ __forceinline__ void int_chunk_loop(float (&acc)[16], const uint8_t *
                                                int64_t ldc, const int32_t *__restrict__ rows,
                                                const float *__restrict__ w, int K, int split,
                                                const FastDiv &d) {
-    constexpr int U = 3;  // clients per batch (two batches in flight per lane)
+    constexpr int U = DLS_QUANT_U;  // clients per batch (two batches in flight per lane)
     const f32x2 zero2 = f32x2{0.f, 0.f};
     {
         const int64_t row = rows[0];
@@ -131,9 +137,16 @@ __device__ __forceinline__ void int_tile(const dls_qtile &t, const uint8_t *__re
     if (t.row_len >= 16) {
         const int split = t.row_len - r;  // elements [0, split) in channel c, rest in c + 1
         // wave-uniform choice: most waves of a large-row tensor never straddle a channel
-        if (__ballot(split < 16) == 0)
-            int_chunk_loop<SIGNED, false>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K, 16, d);
-        else
+        if (__ballot(split < 16) == 0) {
+            const int c0 = __builtin_amdgcn_readfirstlane(c);
+            if (DLS_QUANT_SCALAR_SZ && __ballot(c != c0) == 0)  // one channel for the whole
+                // wave: (scale, zp) become scalar loads and the fast-path test a uniform branch
+                int_chunk_loop<SIGNED, false>(acc, Q + t.src + e0, ldq, sz + c0, ldc, rows, w, K,
+                                              16, d);
+            else
+                int_chunk_loop<SIGNED, false>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K,
+                                              16, d);
+        } else
             int_chunk_loop<SIGNED, true>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K, split, d);
     } else {  // tiny channel rows: per-element channel lookup
         const float zadj = SIGNED ? 128.f : 0.f;

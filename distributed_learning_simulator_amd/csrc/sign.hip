@@ -134,7 +134,13 @@ struct HSCounter {
 // fp32 signs.  Exact: the counters hold K < 8 * 2^CB.
 // 64-thread blocks: one wave per block, so ~P/64/64 waves spread evenly over
 // the 256 CUs (256-thread blocks left 3-vs-2 blocks per CU, a 12% tail).
-constexpr int kVoteBlock = 64;
+#ifndef DLS_VOTE_BLOCK
+#define DLS_VOTE_BLOCK 64
+#endif
+#ifndef DLS_VOTE_DB
+#define DLS_VOTE_DB 1
+#endif
+constexpr int kVoteBlock = DLS_VOTE_BLOCK;
 
 template <int CB>
 __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
@@ -182,6 +188,12 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
         cn.add8(xn);
     };
     u64x2 wa[B8], wb[B8];
+    if (!DLS_VOTE_DB) {
+        for (int j = 0; j < K; j += B8) {
+            load8(j, wa);
+            consume8(wa);
+        }
+    } else {
     load8(0, wa);
     for (int j = 0; j < K; j += 2 * B8) {
         if (j + B8 < K) load8(j + B8, wb);
@@ -189,6 +201,7 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
         if (j + B8 >= K) break;
         if (j + 2 * B8 < K) load8(j + 2 * B8, wa);
         consume8(wb);
+    }
     }
     const int64_t e0 = g * 64;
     const bool full = e0 + 64 <= P;

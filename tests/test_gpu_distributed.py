@@ -1,0 +1,99 @@
+"""GPU: the sharded servers with the real HIP kernels, 2 ranks on one GPU over gloo.
+
+(RCCL needs one GPU per rank, so the single-GPU test box exercises the same
+code path with the gloo backend; the collectives are the same calls.)
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests import golden as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from distributed_learning_simulator_amd.distributed import (ShardedFedQuantServer,
+                                                                ShardedFedServer,
+                                                                ShardedSignSGDServer)
+    out = {}
+    # FedAvg
+    z = G.load("fedavg.npz")
+    case = G.meta(z)[1]
+    k, layout, K = case["key"], case["layout"], case["K"]
+    U, n = z[f"{k}_U"], z[f"{k}_n"]
+    s = ShardedFedServer(tester=None, worker_number=K, synchronous=True)
+    for wid in s.local_worker_ids:
+        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
+        s.worker_data_queue.add_task((wid, int(n[wid]), d))
+    for w in s.local_worker_ids:
+        s.worker_data_queue.get_result(consumer=w, timeout=60)
+    res = s.worker_data_queue.get_result(consumer=s.local_worker_ids[0], timeout=60)
+    out["fed"] = np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout])
+    # sign vote
+    zs = G.load("sign_vote.npz")
+    cs = G.meta(zs)[1]
+    S = zs["c1_signs"]
+    ss = ShardedSignSGDServer(tester=None, worker_number=cs["K"], synchronous=True)
+    for wid in ss.local_worker_ids:
+        ss.worker_data_queue.add_task(
+            [torch.from_numpy(v.copy()) for v in G.split(S[wid], cs["layout"]).values()])
+    res = ss.worker_data_queue.get_result(consumer=0, timeout=60)
+    out["sign"] = np.concatenate([t.reshape(-1).cpu().numpy() for t in res])
+    # fed_quant
+    zq = G.load("dequant.npz")
+    cq = G.meta(zq)[0]
+    sq = ShardedFedQuantServer(tester=None, worker_number=cq["K"], synchronous=True)
+    for i in sq.local_worker_ids:
+        d = {}
+        for name, shape in cq["layout"]:
+            if name in cq["qnames"]:
+                d[name] = tuple(torch.from_numpy(zq[f"q{i}_{name}_{x}"].copy())
+                                for x in ("int", "scale", "zp"))
+            else:
+                d[name] = torch.from_numpy(zq[f"q{i}_{name}_f32"].copy())
+        sq.worker_data_queue.add_task((i, int(zq["n"][i]), d))
+    agg = sq.last_aggregate
+    out["quant"] = np.concatenate([agg[nm].reshape(-1).cpu().numpy() for nm, _ in cq["layout"]])
+    outq.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_sharded_servers_two_ranks_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=170) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    z = G.load("fedavg.npz")
+    k = G.meta(z)[1]["key"]
+    ref = z[f"{k}_full"]
+    for r in (0, 1):
+        got = outs[r]["fed"]
+        assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-6
+        assert np.array_equal(outs[r]["sign"].view(np.uint32),
+                              G.load("sign_vote.npz")["c1_vote"].view(np.uint32))
+        zq = G.load("dequant.npz")
+        assert np.linalg.norm(outs[r]["quant"] - zq["agg"]) / np.linalg.norm(zq["agg"]) < 1e-6
+    assert np.array_equal(outs[0]["fed"].view(np.uint32), outs[1]["fed"].view(np.uint32))

@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Same-process, interleaved A/B timing of libdls_hip.so variants (tools/_variants/).
+
+    python tools/ab_bench.py --workloads fedavg,vote,quant,gemm,pack [--rounds 5]
+
+Each variant library is loaded with its own ctypes handle; every round times
+`--launches` launches of each variant back to back with HIP events, so box /
+clock drift hits all variants alike (cdna_hip_programming.md §5.4 rule 24).
+"""
+import argparse
+import ctypes
+import glob
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from distributed_learning_simulator_amd import _native  # noqa: E402
+from distributed_learning_simulator_amd.layout import ParameterLayout  # noqa: E402
+from distributed_learning_simulator_amd.model_shapes import resnet18_cifar, vgg16  # noqa: E402
+
+P_ = ctypes.c_void_p
+
+
+def load(path):
+    L = ctypes.CDLL(path)
+    for name, (args, res) in _native.SIGNATURES.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def setup(dev):
+    W = {}
+    lay = ParameterLayout(resnet18_cifar())
+    P = lay.P
+    g = torch.Generator(device=dev).manual_seed(1)
+    U = torch.randn((100, P), generator=g, device=dev) * 0.05
+    rows = torch.arange(100, dtype=torch.int32, device=dev)
+    w = torch.randint(100, 1000, (100,), generator=g, device=dev).float()
+    out = torch.empty(P, device=dev)
+    tot = float(w.sum())
+    W["fedavg"] = (lambda L: L.dls_fedavg_f32(ptr(U), P, ptr(rows), ptr(w), 100, tot, P, 0,
+                                              ptr(out), stream()), 100 * P * 4 + P * 4)
+    Wd = _native.sign_words(P)
+    planes = torch.randint(-2**62, 2**62, (1000, Wd), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]
+    so = torch.empty(P, device=dev)
+    cnt = torch.empty(P, dtype=torch.int32, device=dev)
+    W["vote"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, ptr(cnt), ptr(so),
+                                           stream()), 1000 * Wd * 8 + 2 * P * 4)
+    X = torch.sign(torch.randn((16, P), generator=g, device=dev))
+    pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
+    W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
+                 16 * (P * 4 + Wd * 8))
+    from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
+    template = {}
+    for name, s in vgg16():
+        if len(s) >= 2:
+            template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
+                              torch.zeros(s[0], dtype=torch.int64))
+        else:
+            template[name] = torch.zeros(s)
+    st = QuantizedClientStore(template, dev, capacity=100)
+    st.Q.random_(0, 256, generator=g)
+    st.F.normal_(generator=g)
+    st.sz[:, :, 0].uniform_(1e-4, 1e-2, generator=g)
+    st.sz[:, :, 1].zero_()
+    qo = torch.empty(st.layout.P, device=dev)
+    ql = st.qlayout
+    Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
+    Pf = sum(m for m, k in zip(st.layout.numels, ql.kinds) if not k)
+    W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, ptr(st.Q), st.Q.stride(0),
+                                                 ptr(st.F), st.F.stride(0), ptr(st.sz),
+                                                 st.sz.stride(0) // 2, ptr(rows), ptr(w), 100, tot,
+                                                 ptr(qo), stream()),
+                  100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+    C = torch.rand((50, 50), generator=g, device=dev)
+    C = C / C.sum(1, keepdim=True)
+    go = torch.empty((50, P), device=dev)
+    W["gemm"] = (lambda L: L.dls_subset_gemm_f32(ptr(C), 50, 50, ptr(U), P, ptr(rows), P, ptr(go),
+                                                 P, stream()), 100 * P * 4)
+    return W
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workloads", default="fedavg,vote,quant,gemm,pack")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=10)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    libs = {os.path.basename(p)[7:-3]: load(p)
+            for p in sorted(glob.glob(os.path.join(ROOT, "tools", "_variants", "libdls_*.so")))}
+    W = setup(dev)
+    res = {}
+    for wl in args.workloads.split(","):
+        fn, nbytes = W[wl]
+        times = {v: [] for v in libs}
+        for name, L in libs.items():  # warm (and check status)
+            rc = fn(L)
+            assert rc == 0, (wl, name, rc, L.dls_last_error())
+        torch.cuda.synchronize()
+        for _ in range(args.rounds):
+            for name, L in libs.items():
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(args.launches):
+                    fn(L)
+                b.record()
+                b.synchronize()
+                times[name].append(a.elapsed_time(b) / args.launches)
+        for name in libs:
+            ms = statistics.median(times[name])
+            res.setdefault(wl, {})[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
+                                           "min_ms": round(min(times[name]), 4)}
+        print(wl, json.dumps(res[wl]), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Build libdls_hip.so variants with -D knobs for same-box A/B timing (tools/ab_bench.py).
+
+    python tools/build_variants.py base: qU2:-DDLS_QUANT_U=2 noscalar:-DDLS_QUANT_SCALAR_SZ=0
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "distributed_learning_simulator_amd", "csrc")
+OUT = os.path.join(ROOT, "tools", "_variants")
+SRCS = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "shapley.hip"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
+
+
+def build(name, defs):
+    d = os.path.join(OUT, name)
+    os.makedirs(d, exist_ok=True)
+    objs = []
+    for s in SRCS:
+        o = os.path.join(d, s.replace(".hip", ".o"))
+        subprocess.check_call(["hipcc", *FLAGS, *defs, "-c", os.path.join(CSRC, s), "-o", o])
+        objs.append(o)
+    lib = os.path.join(OUT, f"libdls_{name}.so")
+    subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, *objs])
+    return lib
+
+
+def main(specs):
+    jobs = []
+    for spec in specs:
+        name, _, flags = spec.partition(":")
+        jobs.append((name, [f for f in flags.split(",") if f]))
+    with cf.ThreadPoolExecutor(4) as ex:
+        for lib in ex.map(lambda j: build(*j), jobs):
+            print(lib)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
