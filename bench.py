@@ -69,17 +69,18 @@ def timed_launches(fn, steps, warmup, sync_all=None):
     return wall, [a.elapsed_time(b) for a, b in ev]
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+def load_traffic(key):
+    """HBM bytes per launch of this workload's kernel from the committed rocprofv3
+    PMC passes (profiles/pmc_traffic.json, tools/pmc_summary.py), if present."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
 
-def roofline(kernel, bytes_per_launch, kernel_ms, bound="hbm", flops_per_launch=None):
+def roofline(kernel, bytes_per_launch, kernel_ms, bound="hbm", flops_per_launch=None, key=None):
     avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     if bound == "hbm":
         achieved = bytes_per_launch / avg_s / 1e9
@@ -88,7 +89,7 @@ def roofline(kernel, bytes_per_launch, kernel_ms, bound="hbm", flops_per_launch=
         achieved = flops_per_launch / avg_s / 1e12
         peak, unit = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
     return {"kernel": kernel, "bound": bound, "achieved": round(achieved, 2), "peak": peak,
-            "unit": unit, "frac": round(achieved / peak, 4), "traffic": load_traffic(kernel),
+            "unit": unit, "frac": round(achieved / peak, 4), "traffic": load_traffic(key or kernel),
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "avg_launch_us": round(avg_s * 1e6, 2)}
 
@@ -148,7 +149,7 @@ def bench_fedavg(args, dev, rank, world):
     upd_bytes = layout.numel * 4  # one client update (fp32, unpadded)
     value = world * K * upd_bytes / (ms / 1e3) / 1e9
     bytes_per_launch = K * P * 4 + P * 4
-    rf = roofline("dls_fedavg_f32", bytes_per_launch, kms)
+    rf = roofline("dls_fedavg_f32", bytes_per_launch, kms, key="headline")
     if world > 1:  # the events bracket all chunks' kernels (and interleaved RCCL enqueue)
         rf["note"] = "launch window includes chunked all-reduce overlap"
     del U
@@ -179,7 +180,7 @@ def bench_fedavg_k1000(args, dev):
     return {"config": "FedAvg of 1000 ResNet-18 fp32 updates (44.7 GB), bit-exact reference order",
             "value": round(K * layout.numel * 4 / (ms / 1e3) / 1e9, 2), "unit": "GB/s",
             "ms_per_step": round(ms, 4),
-            "roofline": roofline("dls_fedavg_f32", K * P * 4 + P * 4, kms)}
+            "roofline": roofline("dls_fedavg_f32", K * P * 4 + P * 4, kms, key="fedavg_k1000")}
 
 
 def bench_sign(args, dev):
@@ -220,8 +221,9 @@ def bench_sign(args, dev):
         "config": "signSGD majority vote, 1000 clients x ResNet-18 (2-bit planes)",
         "value": round(K * wire / (ms / 1e3) / 1e9, 2), "unit": "GB/s (packed client updates)",
         "fp32_logical_GBps": round(K * layout.numel * 4 / (ms / 1e3) / 1e9, 2),
-        "ms_per_step": round(ms, 4), "roofline": roofline("dls_sign_vote", bytes_per_launch, kms),
-        "pack": roofline("dls_sign_pack_f32", 16 * (P * 4 + W * 8), pkms),
+        "ms_per_step": round(ms, 4),
+        "roofline": roofline("dls_sign_vote", bytes_per_launch, kms, key="sign_vote"),
+        "pack": roofline("dls_sign_pack_f32", 16 * (P * 4 + W * 8), pkms, key="sign_pack"),
     }
 
 
@@ -272,7 +274,7 @@ def bench_quant(args, dev):
         "unit": "GB/s (int8 client updates)",
         "fp32_logical_GBps": round(K * (Pq + Pf) * 4 / (ms / 1e3) / 1e9, 2),
         "ms_per_step": round(ms, 4),
-        "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms),
+        "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms, key="fed_quant"),
     }
 
 
@@ -300,9 +302,9 @@ def bench_shapley_gemm(args, dev):
     ms = wall / args.steps * 1e3
     flops = 2.0 * S * K * layout.numel
     bytes_per_launch = (K + S) * P * 4
-    rf_hbm = roofline("dls_subset_gemm_f32", bytes_per_launch, kms)
+    rf_hbm = roofline("dls_subset_gemm_f32", bytes_per_launch, kms, key="shapley_gemm")
     rf_mfma = roofline("dls_subset_gemm_f32", bytes_per_launch, kms, bound="mfma",
-                       flops_per_launch=flops)
+                       flops_per_launch=flops, key="shapley_gemm")
     del U, out
     return {
         "config": f"Shapley subset aggregation as fp32 MFMA GEMM, {S} subsets x 50 clients x ResNet-18",
@@ -422,6 +424,8 @@ def main():
     ap.add_argument("--quick", action="store_true", help="headline only (no components)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
+    ap.add_argument("--only", default="", help="comma list: headline,fedavg_k1000,sign_vote,"
+                                                "fed_quant,shapley_gemm,shapley_evals")
     ap.add_argument("--cpu-clients", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -439,13 +443,19 @@ def main():
         else:  # dry runs of the N>1 path on a single-GPU box
             dist.init_process_group(args.backend)
 
-    value, ms, rf, extra = bench_fedavg(args, dev, rank, world)
+    only = set(args.only.split(",")) if args.only else None
+    value = ms = rf = None
+    extra = {}
+    if only is None or "headline" in only:
+        value, ms, rf, extra = bench_fedavg(args, dev, rank, world)
     components = {}
     if not args.quick and rank == 0:
         for name, fn in (("fedavg_k1000", bench_fedavg_k1000), ("sign_vote", bench_sign),
                          ("fed_quant", bench_quant),
                          ("shapley_gemm", bench_shapley_gemm),
                          ("shapley_evals", bench_shapley_evals)):
+            if only is not None and name not in only:
+                continue
             try:
                 components[name] = fn(args, dev)
                 log(name, json.dumps(components[name]))
@@ -453,15 +463,17 @@ def main():
                 components[name] = {"error": repr(e)}
             torch.cuda.empty_cache()
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and only is None:
         cpu = cpu_baseline(args)
     if world > 1:
         dist.barrier()
     if rank == 0:
         line = {
             "metric": "client-update GB/s aggregated per FL round",
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "value": round(value, 2) if value is not None else None, "unit": "GB/s",
+            "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4) if ms is not None else None,
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": "FedAvg aggregation of 100 synthetic ResNet-18 (11.2M-param "
                                    "fp32) client updates per GPU, bit-exact reference order",
