@@ -53,8 +53,7 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
     if (tile >= ntiles) return;
-    const int nsteps = Kp / 2;       // multiple of 4 (Kp padded to 8): register ring period
-    const int real_steps = (K + 1) / 2;  // k-steps that hold clients; padded ones skip the MFMAs
+    const int nsteps = Kp / 2;  // multiple of 4 (Kp padded to 8)
 
     // One flattened (tile, k-step) stream: the U loads of the next 4 k-steps are
     // in flight while the MFMAs of the current one run, and across a tile seam
@@ -103,13 +102,13 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
             const bool seam = s + 4 >= nsteps;
             const int64_t lt = seam ? next : tile;
             const int ls = seam ? s + 4 - nsteps : s + 4;
-            if (s < real_steps) mma(s, b0);
+            mma(s, b0);
             b0 = loadB(lt, ls);
-            if (s + 1 < real_steps) mma(s + 1, b1);
+            mma(s + 1, b1);
             b1 = loadB(lt, ls + 1);
-            if (s + 2 < real_steps) mma(s + 2, b2);
+            mma(s + 2, b2);
             b2 = loadB(lt, ls + 2);
-            if (s + 3 < real_steps) mma(s + 3, b3);
+            mma(s + 3, b3);
             b3 = loadB(lt, ls + 3);
         }
         if (inb) {
