@@ -30,21 +30,21 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kTileP = 128;
 constexpr int kMaxK = 256;
 
-template <int MT, bool BETA>
+template <int MT, bool BETA, int kDepth>
 __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict__ C, int64_t ldc, int S, int K,
                                                         const float *__restrict__ U, int64_t ldu,
                                                         const int32_t *__restrict__ rows, int64_t P,
                                                         float *__restrict__ out, int64_t ldo,
                                                         int64_t ntiles) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int Kp = (K + 7) & ~7;  // k-steps of 2 clients, 4 steps per pipeline round
+    const int Kp = ((K + 1) / 2 + kDepth - 1) / kDepth * kDepth * 2;  // whole pipeline rounds
     float *Ct = smem;                                        // [Kp][32*MT]
     int32_t *srow = reinterpret_cast<int32_t *>(smem + Kp * 32 * MT);  // [Kp]
     for (int idx = threadIdx.x; idx < Kp * 32 * MT; idx += kBlock) {
         const int k = idx / (32 * MT), i = idx % (32 * MT);
         Ct[idx] = (k < K && i < S) ? C[(int64_t)i * ldc + k] : 0.f;
     }
-    for (int k = threadIdx.x; k < Kp + 8; k += kBlock) srow[k] = k < K ? rows[k] : -1;
+    for (int k = threadIdx.x; k < Kp + 2 * kDepth; k += kBlock) srow[k] = k < K ? rows[k] : -1;
     __syncthreads();
 
     const int lane = __lane_id();
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
     if (tile >= ntiles) return;
-    const int nsteps = Kp / 2;  // multiple of 4 (Kp padded to 8)
+    const int nsteps = Kp / 2;  // multiple of kDepth
 
     // One flattened (tile, k-step) stream: the U loads of the next 4 k-steps are
     // in flight while the MFMAs of the current one run, and across a tile seam
@@ -66,7 +66,9 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
             b = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + pp));
         return b;
     };
-    f32x4 b0 = loadB(tile, 0), b1 = loadB(tile, 1), b2 = loadB(tile, 2), b3 = loadB(tile, 3);
+    f32x4 b[kDepth];
+#pragma unroll
+    for (int i = 0; i < kDepth; ++i) b[i] = loadB(tile, i);
     for (; tile < ntiles; tile += stride) {
         const int64_t p = tile * kTileP + 4 * col;  // this lane's 4 parameters
         const bool inb = p + 4 <= P;
@@ -98,18 +100,15 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                     acc[mt][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[n], acc[mt][n], 0, 0, 0);
             }
         };
-        for (int s = 0; s < nsteps; s += 4) {
-            const bool seam = s + 4 >= nsteps;
+        for (int s = 0; s < nsteps; s += kDepth) {
+            const bool seam = s + kDepth >= nsteps;
             const int64_t lt = seam ? next : tile;
-            const int ls = seam ? s + 4 - nsteps : s + 4;
-            mma(s, b0);
-            b0 = loadB(lt, ls);
-            mma(s + 1, b1);
-            b1 = loadB(lt, ls + 1);
-            mma(s + 2, b2);
-            b2 = loadB(lt, ls + 2);
-            mma(s + 3, b3);
-            b3 = loadB(lt, ls + 3);
+            const int ls = seam ? s + kDepth - nsteps : s + kDepth;
+#pragma unroll
+            for (int i = 0; i < kDepth; ++i) {
+                mma(s + i, b[i]);
+                b[i] = loadB(lt, ls + i);
+            }
         }
         if (inb) {
 #pragma unroll
@@ -126,11 +125,11 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
     }
 }
 
-template <int MT, bool BETA>
+template <int MT, bool BETA, int kDepth>
 unsigned grid_blocks(int64_t ntiles, size_t lds) {
     // exactly the resident blocks (persistent): every wave gets ntiles/(blocks*4) tiles
     int slot = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&slot, k_subset_gemm<MT, BETA>, kBlock, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&slot, k_subset_gemm<MT, BETA, kDepth>, kBlock, lds) !=
             hipSuccess || slot < 1)
         slot = 1;
     int dev = 0, cus = 256;
@@ -161,21 +160,33 @@ extern "C" int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const f
         const int Sc = S - s0 < 64 ? S - s0 : 64;
         for (int k0 = 0; k0 < K; k0 += kMaxK) {
             const int Kc = K - k0 < kMaxK ? K - k0 : kMaxK;
-            const int Kp = (Kc + 7) & ~7;
+            // pipeline depth (k-steps in flight) 4 or 5: whichever pads K less
+            // (K = 50 -> 25 k-steps = 5 rounds of 5, no padded MFMAs)
+            const int steps = (Kc + 1) / 2;
+            const int depth = ((steps + 4) / 5 * 5 - steps) < ((steps + 3) / 4 * 4 - steps) ? 5 : 4;
+            const int Kp = (steps + depth - 1) / depth * depth * 2;
             const int MT = Sc > 32 ? 2 : 1;
-            const size_t lds = (size_t)Kp * 32 * MT * sizeof(float) + (size_t)(Kp + 8) * sizeof(int32_t);
+            const size_t lds =
+                (size_t)Kp * 32 * MT * sizeof(float) + (size_t)(Kp + 2 * depth) * sizeof(int32_t);
             // C chunk: rows s0.., columns k0.. of the row-major [S, K] matrix (ld K)
             const float *Cc = C + (int64_t)s0 * K + k0;
             const int beta = k0 > 0;
             float *oc = out + (int64_t)s0 * ldo;
-#define DLS_GEMM_LAUNCH(MT_, B_)                                                              \
-    hipLaunchKernelGGL((k_subset_gemm<MT_, B_>), dim3(grid_blocks<MT_, B_>(ntiles, lds)),      \
-                       dim3(kBlock), lds, st, Cc, (int64_t)K, Sc, Kc, U, ldu, rows + k0, P, oc,  \
+#define DLS_GEMM_LAUNCH(MT_, B_, D_)                                                            \
+    hipLaunchKernelGGL((k_subset_gemm<MT_, B_, D_>), dim3(grid_blocks<MT_, B_, D_>(ntiles, lds)), \
+                       dim3(kBlock), lds, st, Cc, (int64_t)K, Sc, Kc, U, ldu, rows + k0, P, oc,    \
                        ldo, ntiles)
-            if (MT == 2 && beta) DLS_GEMM_LAUNCH(2, true);
-            else if (MT == 2) DLS_GEMM_LAUNCH(2, false);
-            else if (beta) DLS_GEMM_LAUNCH(1, true);
-            else DLS_GEMM_LAUNCH(1, false);
+#define DLS_GEMM_MT_BETA(D_)                    \
+    if (MT == 2 && beta) DLS_GEMM_LAUNCH(2, true, D_);   \
+    else if (MT == 2) DLS_GEMM_LAUNCH(2, false, D_);     \
+    else if (beta) DLS_GEMM_LAUNCH(1, true, D_);         \
+    else DLS_GEMM_LAUNCH(1, false, D_);
+            if (depth == 5) {
+                DLS_GEMM_MT_BETA(5)
+            } else {
+                DLS_GEMM_MT_BETA(4)
+            }
+#undef DLS_GEMM_MT_BETA
 #undef DLS_GEMM_LAUNCH
             int rc = check_launch("dls_subset_gemm_f32");
             if (rc) return rc;

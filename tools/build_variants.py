@@ -15,13 +15,13 @@ SRCS = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "shapley.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
 
-def build(name, defs):
+def build(name, defs, src=CSRC):
     d = os.path.join(OUT, name)
     os.makedirs(d, exist_ok=True)
     objs = []
     for s in SRCS:
         o = os.path.join(d, s.replace(".hip", ".o"))
-        subprocess.check_call(["hipcc", *FLAGS, *defs, "-c", os.path.join(CSRC, s), "-o", o])
+        subprocess.check_call(["hipcc", *FLAGS, *defs, "-I", CSRC, "-c", os.path.join(src, s), "-o", o])
         objs.append(o)
     lib = os.path.join(OUT, f"libdls_{name}.so")
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, *objs])
@@ -29,10 +29,20 @@ def build(name, defs):
 
 
 def main(specs):
+    """spec = name:flag,flag[@git-rev]  (@rev builds the csrc of that git revision)"""
     jobs = []
     for spec in specs:
+        spec, _, rev = spec.partition("@")
         name, _, flags = spec.partition(":")
-        jobs.append((name, [f for f in flags.split(",") if f]))
+        src = CSRC
+        if rev:
+            src = os.path.join(OUT, f"_src_{rev}")
+            os.makedirs(src, exist_ok=True)
+            for f in SRCS + ["dls_common.h"]:
+                blob = subprocess.check_output(
+                    ["git", "-C", ROOT, "show", f"{rev}:distributed_learning_simulator_amd/csrc/{f}"])
+                open(os.path.join(src, f), "wb").write(blob)
+        jobs.append((name, [f for f in flags.split(",") if f], src))
     with cf.ThreadPoolExecutor(4) as ex:
         for lib in ex.map(lambda j: build(*j), jobs):
             print(lib)
