@@ -183,3 +183,68 @@ class ShardedSignSGDServer(SignSGDServer):
         super()._ensure(shapes)
         if first and self._planes.shape[0] != len(self.local_worker_ids):
             self._planes = self._planes[: max(1, len(self.local_worker_ids))].contiguous()
+
+
+class _ShardedShapleyMixin(_ShardedMixin):
+    """Shapley servers on several ranks: each rank receives its own
+    clients' updates, one all-gather per round gives every rank all K client rows
+    (RCCL over xGMI), then the coalitions of every evaluation batch are dealt
+    round-robin over the ranks (``ShapleyValueServer.evaluate_subsets``)."""
+
+    def _gather_clients(self):
+        store = self.parameters.store
+        P = store.layout.P
+        local = list(self.parameters.keys())
+        kmax = max(1, -(-self.worker_number // self.world_size))
+        buf = torch.zeros((kmax, P), dtype=torch.float32, device=self.device)
+        meta = torch.full((kmax, 2), -1, dtype=torch.int64, device=self.device)
+        for j, wid in enumerate(local):
+            buf[j].copy_(store.row(self.parameters.row_of(wid)))
+            meta[j, 0] = wid
+            meta[j, 1] = self.parameters.n_of(wid)
+        bufs = [torch.empty_like(buf) for _ in range(self.world_size)]
+        metas = [torch.empty_like(meta) for _ in range(self.world_size)]
+        dist.all_gather(bufs, buf, group=self.group)
+        dist.all_gather(metas, meta, group=self.group)
+        incoming = {}
+        for b, m in zip(bufs, metas):
+            for j, (wid, n) in enumerate(m.tolist()):
+                if wid >= 0:
+                    incoming[wid] = (n, b[j])
+        # every rank now holds all K clients, in worker-id order
+        for wid in list(self.parameters.keys()):
+            del self.parameters[wid]
+        for wid in sorted(incoming):
+            n, row = incoming[wid]
+            self.parameters[wid] = (n, store.layout.views(row))
+
+    def _before_aggregate(self):
+        self._gather_clients()
+
+
+def _sharded_shapley(cls):
+    class Sharded(_ShardedShapleyMixin, cls):
+        def __init__(self, group=None, **kwargs):
+            self._init_shard(kwargs["worker_number"], group, 1)
+            super().__init__(**kwargs)
+
+    Sharded.__name__ = "Sharded" + cls.__name__
+    Sharded.__qualname__ = Sharded.__name__
+    return Sharded
+
+
+from .servers.GTG_shapley_value_server import GTGShapleyValueServer  # noqa: E402
+from .servers.multiround_shapley_value_server import MultiRoundShapleyValueServer  # noqa: E402
+
+ShardedGTGShapleyValueServer = _sharded_shapley(GTGShapleyValueServer)
+ShardedMultiRoundShapleyValueServer = _sharded_shapley(MultiRoundShapleyValueServer)
+
+
+def get_sharded_server(algorithm, **kwargs):
+    """factory.get_server for one process per GPU (torch.distributed initialised)."""
+    table = {"fed": ShardedFedServer, "fed_quant": ShardedFedQuantServer,
+             "sign_SGD": ShardedSignSGDServer, "GTG_shapley_value": ShardedGTGShapleyValueServer,
+             "multiround_shapley_value": ShardedMultiRoundShapleyValueServer}
+    if algorithm not in table:
+        raise RuntimeError("unknown algorithm:" + algorithm)
+    return table[algorithm](**kwargs)

@@ -11,7 +11,15 @@ from .workers.sign_sgd_worker import SignSGDWorker
 from .workers.worker import Worker
 
 
-def get_server(algorithm, **kwargs) -> Server:
+def get_server(algorithm, sharded=None, **kwargs) -> Server:
+    """factory.py:14-25.  ``sharded`` (default: torch.distributed initialised with
+    more than one rank) returns the one-process-per-GPU servers of distributed.py."""
+    if sharded is None:
+        import torch.distributed as dist
+        sharded = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if sharded:
+        from .distributed import get_sharded_server
+        return get_sharded_server(algorithm, **kwargs)
     if algorithm == "sign_SGD":
         return SignSGDServer(**kwargs)
     if algorithm == "fed_quant":

@@ -61,6 +61,9 @@ class FedServer(Server):
     def _process_client_parameter(self, client_parameter: dict):
         return client_parameter
 
+    def _before_aggregate(self):
+        """Hook when this process has all its clients of the round (sharded servers)."""
+
     def _process_aggregated_parameter(self, aggregated_parameter: dict):
         return aggregated_parameter
 
@@ -86,6 +89,7 @@ class FedServer(Server):
         if len(self.parameters) != self.clients_per_round:
             log.debug("%s %s,skip", len(self.parameters), self.clients_per_round)
             return None
+        self._before_aggregate()
         self.round += 1
         log.info("begin aggregating")
         avg_parameter = self.get_subset_model(self.parameters.keys())

@@ -140,3 +140,38 @@ def test_shapley_fanout_two_ranks():
         for k, v in case["sv"].items():
             assert abs(sv[int(k)] - v) <= 1e-12
     assert out[0][2] + out[1][2] == len(case["evaluated"])  # the evaluations were split
+
+
+def _sharded_gtg_worker(rank, world, port, outq):
+    _init(rank, world, port)
+    from distributed_learning_simulator_amd import factory
+    case = next(c for c in G.shapley_cases() if c["tag"] == "gtg_6_3")
+    layout = [(nm, tuple(s)) for nm, s in case["layout"]]
+    K = case["K"]
+    U = np.array(case["U"], np.float32)
+    target = np.array(case["target"], np.float64)
+    server = factory.get_server("GTG_shapley_value", tester=None, worker_number=K,
+                                synchronous=True, device=torch.device("cpu"))
+    assert type(server).__name__ == "ShardedGTGShapleyValueServer"
+    server._set_prev_model(G.split(torch.tensor(case["prev"]), layout))
+
+    def util(model, metric_type="acc"):
+        v = np.concatenate([np.asarray(model[nm], np.float64).reshape(-1) for nm, _ in layout])
+        d = v - target
+        return float(1.0 / (1.0 + float(np.dot(d, d)) / case["scale"]))
+
+    server.get_metric = util
+    np.random.seed(case["seed"])
+    for i in server.local_worker_ids:  # each rank only receives its own clients
+        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[i], layout).items()}
+        server.worker_data_queue.add_task((i, int(case["n"][i]), d))
+    outq.put((rank, {int(k): float(v) for k, v in server.shapley_values[1].items()}, 0))
+    dist.destroy_process_group()
+
+
+def test_sharded_gtg_two_ranks_clients_sharded():
+    case = next(c for c in G.shapley_cases() if c["tag"] == "gtg_6_3")
+    out = _spawn(_sharded_gtg_worker)
+    for _, sv, _n in out:
+        for k, v in case["sv"].items():
+            assert abs(sv[int(k)] - v) <= 1e-12
