@@ -255,8 +255,8 @@ def bench_quant(args, dev):
     def step(a=None, b=None):
         if a is not None:
             a.record()
-        _native.dequant_fedavg(store.tiles, store.ntiles, store.Q, store.F, store.sz, rows_t, w_t,
-                               total, out)
+        _native.dequant_fedavg(store.tiles, store.ntiles, store.nfast, store.Q, store.F, store.sz,
+                               rows_t, w_t, total, out)
         if b is not None:
             b.record()
 

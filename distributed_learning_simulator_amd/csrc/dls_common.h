@@ -32,6 +32,10 @@ void set_error(const char *fmt, ...);
 // at the caller's next synchronisation).
 int check_launch(const char *what);
 
+// Blocks of `kernel` resident on the whole device at once (occupancy x CUs),
+// for persistent grids; cached per (kernel, device, block, lds).
+int resident_blocks(const void *kernel, int block, size_t lds);
+
 inline hipStream_t as_stream(dls_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 

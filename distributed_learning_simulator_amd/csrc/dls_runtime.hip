@@ -3,7 +3,9 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "dls_common.h"
 
@@ -27,6 +29,33 @@ int check_launch(const char *what) {
         return (int)e;
     }
     return DLS_OK;
+}
+
+int resident_blocks(const void *kernel, int block, size_t lds) {
+    // (kernel, device) -> blocks per CU x CUs; cached: the occupancy query costs
+    // microseconds and the launch functions run on every aggregation
+    static std::mutex mu;
+    static std::unordered_map<std::string, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    char key[96];
+    snprintf(key, sizeof(key), "%p/%d/%d/%zu", kernel, dev, block, lds);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+        cus = 256;
+    const int n = per_cu * cus;
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = n;
+    return n;
 }
 
 }  // namespace dls

@@ -19,6 +19,12 @@ constexpr int kBlock = 256;
 #ifndef DLS_FEDAVG_UNROLL
 #define DLS_FEDAVG_UNROLL 8
 #endif
+#ifndef DLS_FEDAVG_PIPE
+#define DLS_FEDAVG_PIPE 1
+#endif
+#ifndef DLS_FEDAVG_PIPE_U
+#define DLS_FEDAVG_PIPE_U 4
+#endif
 
 template <bool NT>
 __device__ __forceinline__ f32x4 load4(const f32x4 *p) {
@@ -73,6 +79,83 @@ __global__ __launch_bounds__(kBlock) void k_fedavg_exact(const f32x4 *__restrict
     }
     for (; j < K; ++j) acc = add4(acc, term4(load4<NT>(U + (int64_t)rows[j] * ldu4 + i), w[j], d));
     out[i] = acc;
+}
+
+// Software-pipelined form.  Clients are taken in chunks of 64: lane j holds
+// client (base + j)'s row and weight (one coalesced vector load per field per
+// chunk, the next chunk's fetched a whole chunk ahead) and every step reads them
+// back as wave-uniform values with v_readlane, so no s_load -> s_waitcnt sits
+// on the critical path.  Inside a chunk, batches of U clients are
+// double-buffered: batch b+1's U loads are issued before batch b is reduced.
+// Same op sequence as k_fedavg_exact.
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_fedavg_exact_pipe(const f32x4 *__restrict__ Uv,
+                                                              int64_t ldu4,
+                                                              const int32_t *__restrict__ rows,
+                                                              const float *__restrict__ w, int K,
+                                                              FastDiv d, int64_t P4,
+                                                              f32x4 *__restrict__ out) {
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = i0 < P4;
+    const int64_t i = valid ? i0 : P4 - 1;  // every lane stays: the table needs all 64
+    const int lane = __lane_id();
+    // -0 + t == t for every fp32 t (including -0 and NaN), so starting from -0
+    // and always adding reproduces "the first client is assigned"
+    // (servers/fed_server.py:62-65) without a special first step.
+    f32x4 acc = f32x4{-0.f, -0.f, -0.f, -0.f};
+    int nr = rows[min(lane, K - 1)];
+    float nw = w[min(lane, K - 1)];
+    for (int base = 0; base < K; base += 64) {
+        const int tr = nr;
+        const float tw = nw;
+        const int kn = min(base + 64 + lane, K - 1);
+        nr = rows[kn];  // next chunk, in flight behind this one's loads
+        nw = w[kn];
+        const int n = min(64, K - base);
+        auto load = [&](int j0, f32x4 (&x)[U], float (&wk)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = __builtin_amdgcn_readlane(tr, j0 + u);
+                wk[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j0 + u));
+                x[u] = load4<NT>(Uv + r * ldu4 + i);
+            }
+        };
+        auto consume = [&](const f32x4 (&x)[U], const float (&wk)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc = add4(acc, term4(x[u], wk[u], d));
+        };
+        // loads inside the steady-state loop are unconditional, so every consume
+        // waits with an exact vmcnt (a conditional load would make the compiler's
+        // merged count wait for the younger batch too)
+        const int nb = n / U;
+        int j = 0;
+        if (nb > 0) {
+            f32x4 xA[U], xB[U];
+            float wA[U], wB[U];
+            load(0, xA, wA);
+            int b = 0;
+            for (; b + 2 < nb; b += 2) {
+                load((b + 1) * U, xB, wB);
+                consume(xA, wA);
+                load((b + 2) * U, xA, wA);
+                consume(xB, wB);
+            }
+            if (b + 1 < nb) {
+                load((b + 1) * U, xB, wB);
+                consume(xA, wA);
+                consume(xB, wB);
+            } else {
+                consume(xA, wA);
+            }
+            j = nb * U;
+        }
+        for (; j < n; ++j) {
+            const int64_t r = __builtin_amdgcn_readlane(tr, j);
+            const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
+            acc = add4(acc, term4(load4<NT>(Uv + r * ldu4 + i), wk, d));
+        }
+    }
+    if (valid) out[i] = acc;
 }
 
 template <int UNROLL, bool NT>
@@ -158,9 +241,14 @@ extern "C" int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows,
     hipStream_t st = as_stream(stream);
     if (mode == DLS_FEDAVG_EXACT) {
         const FastDiv d = make_fastdiv(total);
-        hipLaunchKernelGGL((k_fedavg_exact<DLS_FEDAVG_UNROLL, true>), grid, dim3(kBlock), 0, st,
-                           reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, d,
-                           P4, reinterpret_cast<f32x4 *>(out));
+        if (DLS_FEDAVG_PIPE)
+            hipLaunchKernelGGL((k_fedavg_exact_pipe<DLS_FEDAVG_PIPE_U, true>), grid, dim3(kBlock), 0,
+                               st, reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight,
+                               (int)K, d, P4, reinterpret_cast<f32x4 *>(out));
+        else
+            hipLaunchKernelGGL((k_fedavg_exact<DLS_FEDAVG_UNROLL, true>), grid, dim3(kBlock), 0, st,
+                               reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K,
+                               d, P4, reinterpret_cast<f32x4 *>(out));
     } else if (mode == DLS_FEDAVG_FMA) {
         hipLaunchKernelGGL((k_fedavg_fma<8, true>), grid, dim3(kBlock), 0, st,
                            reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, total,

@@ -8,6 +8,8 @@
 // materialises the fp32 client tensors:
 //     out[e] (+)= fl(fl(fl(fl(q - zp[c]) * fl32(scale[c])) * fl32(n_i)) / fl32(N))
 // bit-exact in client order.  Algorithmic bytes: K*(Pq + 4*Pf + 8*C) + 4*P.
+#include <type_traits>
+
 #include "dls_common.h"
 
 namespace dls {
@@ -15,10 +17,10 @@ namespace {
 
 constexpr int kBlock = 256;
 #ifndef DLS_QUANT_U
-#define DLS_QUANT_U 2  // A/B on MI355X: 2 > 3 > 4 clients per batch (tools/ab_bench.py)
+#define DLS_QUANT_U 2  // clients per batch; two batches in flight per lane
 #endif
-#ifndef DLS_QUANT_SCALAR_SZ
-#define DLS_QUANT_SCALAR_SZ 1
+#ifndef DLS_QUANT_SCHED
+#define DLS_QUANT_SCHED 2  // element pairs between scheduling barriers (0: none)
 #endif
 
 __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
@@ -30,154 +32,246 @@ __device__ __forceinline__ bool scale_fast(float sw) {
     return sw >= 0x1p-59f && sw <= 0x1p50f;
 }
 
-// One client's contribution to a lane's 16 consecutive elements.  TWO: the
-// chunk straddles a channel boundary at `split` (elements [split,16) use the
-// next channel's (scale, zero point)); FIRST: assign instead of accumulate
-// (servers/fed_server.py:62-65).  The exact-division fast path is decided once
-// per client from the channel scale (scale_fast), not per element.
-template <bool SIGNED, bool TWO, bool FIRST>
-__device__ __forceinline__ void accum16(float (&acc)[16], u32x4 qv, f32x2 a, f32x2 b, float wk,
-                                        int split, const FastDiv &d) {
-    if (SIGNED) qv ^= 0x80808080u;  // int8 q read as the unsigned byte q + 128
-    const float zadj = SIGNED ? 128.f : 0.f;
-    const float za = a.y + zadj, zb = b.y + zadj;
-    const bool fast = d.fast && scale_fast(a.x * wk) && (!TWO || scale_fast(b.x * wk));
-    if (__builtin_expect(fast, 1)) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const bool second = TWO && j >= split;
-            const float s = second ? b.x : a.x;
-            const float z = second ? zb : za;
-            const float x = byte_f32(qv[j >> 2], j & 3);
-            const float q = markstein(((x - z) * s) * wk, d.b, d.y);
-            acc[j] = FIRST ? q : acc[j] + q;
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+    return __builtin_elementwise_fma(a, b, c);
+}
+
+__device__ __forceinline__ int readlane_i(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ float readlane_f(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// --------------------------------------------------------- client pipeline
+// Clients are walked in chunks of 64.  Lane j holds client (base + j)'s row
+// and weight (one coalesced vector load per field and chunk, fetched a chunk
+// ahead), read back as wave-uniform values with v_readlane, so no scalar load
+// sits on the streaming loop's critical path.  Within a chunk, batches of U
+// clients are double-buffered: batch b+1's loads are issued before batch b is
+// reduced.  Loads inside the steady-state loop are unconditional, so every
+// reduction waits with an exact vmcnt.  All 64 lanes must run this (no lane
+// may have exited early).
+template <int U, class Batch, class Load, class Consume, class Single>
+__device__ __forceinline__ void chunk_pipeline(int n, Load load, Consume consume, Single single) {
+    const int nb = n / U;
+    int j = 0;
+    if (nb > 0) {
+        Batch A, B;
+        load(0, A);
+        int b = 0;
+        for (; b + 2 < nb; b += 2) {
+            load((b + 1) * U, B);
+            consume(A);
+            load((b + 2) * U, A);
+            consume(B);
         }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const bool second = TWO && j >= split;
-            const float s = second ? b.x : a.x;
-            const float z = second ? zb : za;
-            const float x = byte_f32(qv[j >> 2], j & 3);
-            const float q = (((x - z) * s) * wk) / d.b;
-            acc[j] = FIRST ? q : acc[j] + q;
+        if (b + 1 < nb) {
+            load((b + 1) * U, B);
+            consume(A);
+            consume(B);
+        } else {
+            consume(A);
         }
+        j = nb * U;
+    }
+    for (; j < n; ++j) single(j);
+}
+
+struct ChunkRows {
+    int r0, r1, r2;   // rows of chunks c, c+1, c+2 (lane j: client 64c + j)
+    float w0, w1, w2;
+    __device__ __forceinline__ void fetch(const int32_t *rows, const float *w, int K, int k,
+                                          int &r, float &wk) {
+        const int kk = min(k + __lane_id(), K - 1);  // past the end: harmless duplicates
+        r = rows[kk];
+        wk = w[kk];
+    }
+    __device__ __forceinline__ void init(const int32_t *rows, const float *w, int K) {
+        fetch(rows, w, K, 0, r0, w0);
+        fetch(rows, w, K, 64, r1, w1);
+        fetch(rows, w, K, 128, r2, w2);
+    }
+    __device__ __forceinline__ void advance(const int32_t *rows, const float *w, int K, int base) {
+        r0 = r1;
+        w0 = w1;
+        r1 = r2;
+        w1 = w2;
+        fetch(rows, w, K, base + 192, r2, w2);
+    }
+};
+
+// ------------------------------------------------------------ int8 tiles
+// One client's contribution to a lane's 16 consecutive elements of ONE channel
+// (wave-uniform scale s and zero point z, already offset by 128 for int8 read
+// as q ^ 0x80).  Packed fp32: every op below is a v_pk_*_f32 over two
+// elements with the scalar ops' IEEE roundings.  When fl(z*s) is exact (always
+// for symmetric int8, z = 128), fl((x - z)*s) == fma(x, s, -z*s): one op.
+template <bool ZFMA, bool FAST>
+__device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s, float zs, float z,
+                                            float wk, const FastDiv &d) {
+    const f32x2 s2 = f32x2{s, s}, w2 = f32x2{wk, wk};
+    const f32x2 nzs = f32x2{-zs, -zs}, z2 = f32x2{z, z};
+    const f32x2 b2 = f32x2{d.b, d.b}, y2 = f32x2{d.y, d.y};
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+        const f32x2 x = f32x2{byte_f32(qv[j >> 2], j & 3), byte_f32(qv[j >> 2], (j + 1) & 3)};
+        const f32x2 deq = ZFMA ? pk_fma(x, s2, nzs) : (x - z2) * s2;
+        const f32x2 t = deq * w2;
+        f32x2 q;
+        if (FAST) {
+            const f32x2 q0 = t * y2;
+            q = pk_fma(pk_fma(-q0, b2, t), y2, q0);
+        } else {
+            q = f32x2{t.x / d.b, t.y / d.b};
+        }
+        const f32x2 r = f32x2{acc[j], acc[j + 1]} + q;
+        acc[j] = r.x;
+        acc[j + 1] = r.y;
+#if DLS_QUANT_SCHED > 0
+        // keep the scheduler from widening the chain over all 16 elements of
+        // every in-flight client (that costs ~60 VGPRs and waves per SIMD)
+        if ((j / 2) % DLS_QUANT_SCHED == DLS_QUANT_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
-template <bool SIGNED, bool TWO>
-__device__ __forceinline__ void int_chunk_loop(float (&acc)[16], const uint8_t *__restrict__ Qt,
-                                               int64_t ldq, const f32x2 *__restrict__ szc,
-                                               int64_t ldc, const int32_t *__restrict__ rows,
-                                               const float *__restrict__ w, int K, int split,
-                                               const FastDiv &d) {
-    constexpr int U = DLS_QUANT_U;  // clients per batch (two batches in flight per lane)
-    const f32x2 zero2 = f32x2{0.f, 0.f};
-    {
-        const int64_t row = rows[0];
-        const u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
-        const f32x2 a = szc[row * ldc];
-        const f32x2 b = TWO ? szc[row * ldc + 1] : zero2;
-        accum16<SIGNED, TWO, true>(acc, qv, a, b, w[0], split, d);
-    }
-    // batches of U clients, double-buffered: batch b+1 loads while batch b computes
+template <bool SIGNED>
+__device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t *__restrict__ Qt,
+                                                int64_t ldq, const f32x2 *__restrict__ szc,
+                                                int64_t ldc, const int32_t *__restrict__ rows,
+                                                const float *__restrict__ w, int K,
+                                                const FastDiv &d) {
+    constexpr int U = DLS_QUANT_U;
     struct Batch {
         u32x4 qv[U];
-        f32x2 a[U], b[U];
+        float s[U], z[U], wk[U];
     };
-    auto load = [&](int k0, Batch &bt) {
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    f32x2 nsz = szc[(int64_t)cr.r0 * ldc];  // this wave's channel, client 64c + lane
+    const float zadj = SIGNED ? 128.f : 0.f;
+    auto one = [&](const u32x4 qv, float s, float z, float wk) {
+        const float zs = z * s;
+        const bool zfma = __builtin_fmaf(z, s, -zs) == 0.f;  // fl(z*s) exact
+        const bool fast = d.fast && scale_fast(s * wk);
+        if (__builtin_expect(zfma && fast, 1))
+            accum16_one<true, true>(acc, qv, s, zs, z, wk, d);
+        else if (fast)
+            accum16_one<false, true>(acc, qv, s, zs, z, wk, d);
+        else
+            accum16_one<false, false>(acc, qv, s, zs, z, wk, d);
+    };
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        const f32x2 tsz = nsz;
+        nsz = szc[(int64_t)cr.r1 * ldc];  // next chunk (its rows landed a chunk ago)
+        cr.advance(rows, w, K, base);
+        const int n = min(64, K - base);
+        // one wave-uniform decision per chunk: if every client of the chunk takes
+        // the common path (exact fl(z*s) and the fast division), the streaming loop
+        // carries that path alone (fewer registers, no per-client branch)
+        const float ls = tsz.x, lz = tsz.y + zadj, lzs = lz * ls;
+        const bool lfast = __builtin_fmaf(lz, ls, -lzs) == 0.f && d.fast && scale_fast(ls * tw);
+        const bool allfast = __ballot(!lfast && __lane_id() < n) == 0;
+        auto fetch = [&](int j, u32x4 &qv, float &sc, float &z, float &wk) {
+            const int64_t r = readlane_i(tr, j);
+            qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
+            if (SIGNED) qv ^= 0x80808080u;  // int8 q read as the unsigned byte q + 128
+            wk = readlane_f(tw, j);
+            sc = readlane_f(tsz.x, j);
+            z = readlane_f(tsz.y, j) + zadj;
+        };
+        auto run = [&](auto common_only) {
+            auto step = [&](const u32x4 qv, float sc, float z, float wk) {
+                if constexpr (decltype(common_only)::value)
+                    accum16_one<true, true>(acc, qv, sc, z * sc, z, wk, d);
+                else
+                    one(qv, sc, z, wk);
+            };
+            chunk_pipeline<U, Batch>(
+                n,
+                [&](int j0, Batch &bt) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t row = rows[k0 + u];
-            bt.qv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
-            bt.a[u] = szc[row * ldc];
-            bt.b[u] = TWO ? szc[row * ldc + 1] : zero2;
-        }
-    };
-    auto consume = [&](int k0, const Batch &bt) {
+                    for (int u = 0; u < U; ++u) fetch(j0 + u, bt.qv[u], bt.s[u], bt.z[u], bt.wk[u]);
+                },
+                [&](const Batch &bt) {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            accum16<SIGNED, TWO, false>(acc, bt.qv[u], bt.a[u], bt.b[u], w[k0 + u], split, d);
-    };
-    int k = 1;
-    const int nfull = (K - 1) / U;  // full batches after the peeled first client
-    if (nfull > 0) {
-        Batch A, B;
-        load(k, A);
-        for (int bi = 0; bi < nfull; bi += 2) {
-            if (bi + 1 < nfull) load(k + U, B);
-            consume(k, A);
-            k += U;
-            if (bi + 1 >= nfull) break;
-            if (bi + 2 < nfull) load(k + U, A);
-            consume(k, B);
-            k += U;
-        }
-    }
-    for (; k < K; ++k) {
-        const int64_t row = rows[k];
-        const u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + row * ldq));
-        const f32x2 a = szc[row * ldc];
-        const f32x2 b = TWO ? szc[row * ldc + 1] : zero2;
-        accum16<SIGNED, TWO, false>(acc, qv, a, b, w[k], split, d);
+                    for (int u = 0; u < U; ++u) step(bt.qv[u], bt.s[u], bt.z[u], bt.wk[u]);
+                },
+                [&](int j) {
+                    u32x4 qv;
+                    float sc, z, wk;
+                    fetch(j, qv, sc, z, wk);
+                    step(qv, sc, z, wk);
+                });
+        };
+        if (allfast)
+            run(std::true_type{});
+        else
+            run(std::false_type{});
     }
 }
 
-// Integer (per-channel) tile: 16 consecutive elements per lane.
+// Lanes of the wave in different channels (and a lane possibly straddling a
+// channel boundary at `split`): per-lane (scale, zero point) loads.
 template <bool SIGNED>
-__device__ __forceinline__ void int_tile(const dls_qtile &t, const uint8_t *__restrict__ Q,
-                                         int64_t ldq, const f32x2 *__restrict__ sz, int64_t ldc,
-                                         const int32_t *__restrict__ rows,
-                                         const float *__restrict__ w, int K, const FastDiv &d,
-                                         float *__restrict__ out, int e0) {
-    const int p = t.row_pos + e0;
-    const int c = t.chan0 + p / t.row_len;
-    const int r = p % t.row_len;
-    float acc[16];
-    if (t.row_len >= 16) {
-        const int split = t.row_len - r;  // elements [0, split) in channel c, rest in c + 1
-        // wave-uniform choice: most waves of a large-row tensor never straddle a channel
-        if (__ballot(split < 16) == 0) {
-            const int c0 = __builtin_amdgcn_readfirstlane(c);
-            if (DLS_QUANT_SCALAR_SZ && __ballot(c != c0) == 0)  // one channel for the whole
-                // wave: (scale, zp) become scalar loads and the fast-path test a uniform branch
-                int_chunk_loop<SIGNED, false>(acc, Q + t.src + e0, ldq, sz + c0, ldc, rows, w, K,
-                                              16, d);
-            else
-                int_chunk_loop<SIGNED, false>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K,
-                                              16, d);
-        } else
-            int_chunk_loop<SIGNED, true>(acc, Q + t.src + e0, ldq, sz + c, ldc, rows, w, K, split, d);
-    } else {  // tiny channel rows: per-element channel lookup
-        const float zadj = SIGNED ? 128.f : 0.f;
-        int cj[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) cj[j] = min(c + (r + j) / t.row_len, t.chan_end - 1);
-        for (int k = 0; k < K; ++k) {
-            const int64_t row = rows[k];
-            u32x4 qv = *reinterpret_cast<const u32x4 *>(Q + row * ldq + t.src + e0);
+__device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_t *__restrict__ Qt,
+                                                  int64_t ldq, const f32x2 *__restrict__ szc,
+                                                  int64_t ldc, int split,
+                                                  const int32_t *__restrict__ rows,
+                                                  const float *__restrict__ w, int K,
+                                                  const FastDiv &d) {
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    const float zadj = SIGNED ? 128.f : 0.f;
+    const bool two = split < 16;
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        cr.advance(rows, w, K, base);
+        const int n = min(64, K - base);
+        for (int j = 0; j < n; ++j) {
+            const int64_t r = readlane_i(tr, j);
+            const float wk = readlane_f(tw, j);
+            u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
             if (SIGNED) qv ^= 0x80808080u;
-            const float wk = w[k];
+            const f32x2 a = szc[r * ldc];
+            const f32x2 b = two ? szc[r * ldc + 1] : a;
+            const float za = a.y + zadj, zb = b.y + zadj;
+            const bool fast = d.fast && scale_fast(a.x * wk) && scale_fast(b.x * wk);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const f32x2 a = sz[row * ldc + cj[j]];
-                const float x = byte_f32(qv[j >> 2], j & 3);
-                const float deq = (x - (a.y + zadj)) * a.x;
-                const float tn = deq * wk;
-                const float q = (d.fast && scale_fast(a.x * wk)) ? markstein(tn, d.b, d.y)
-                                                                : tn / d.b;
-                acc[j] = (k == 0) ? q : acc[j] + q;
+            for (int e = 0; e < 16; ++e) {
+                const bool second = e >= split;
+                const float s = second ? b.x : a.x;
+                const float z = second ? zb : za;
+                const float t = ((byte_f32(qv[e >> 2], e & 3) - z) * s) * wk;
+                acc[e] += fast ? markstein(t, d.b, d.y) : t / d.b;
             }
         }
     }
-    if (e0 + 16 > t.len) {  // tensor tail: keep the row padding zero
+}
+
+// Channel rows shorter than 16 elements: per-element channel lookup.
+template <bool SIGNED>
+__device__ __forceinline__ void int_tiny_rows(float (&acc)[16], const uint8_t *__restrict__ Qt,
+                                              int64_t ldq, const f32x2 *__restrict__ sz,
+                                              int64_t ldc, const int (&cj)[16],
+                                              const int32_t *__restrict__ rows,
+                                              const float *__restrict__ w, int K,
+                                              const FastDiv &d) {
+    const float zadj = SIGNED ? 128.f : 0.f;
+    for (int k = 0; k < K; ++k) {
+        const int64_t row = rows[k];
+        u32x4 qv = *reinterpret_cast<const u32x4 *>(Qt + row * ldq);
+        if (SIGNED) qv ^= 0x80808080u;
+        const float wk = w[k];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = (e0 + j < t.len) ? acc[j] : 0.f;
+        for (int e = 0; e < 16; ++e) {
+            const f32x2 a = sz[row * ldc + cj[e]];
+            const float t = ((byte_f32(qv[e >> 2], e & 3) - (a.y + zadj)) * a.x) * wk;
+            acc[e] += (d.fast && scale_fast(a.x * wk)) ? markstein(t, d.b, d.y) : t / d.b;
+        }
     }
-    f32x4 *o = reinterpret_cast<f32x4 *>(out + t.dst + e0);
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-        o[v] = f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
 }
 
 __device__ __forceinline__ float fp_term(float x, float wk, const FastDiv &d) {
@@ -185,48 +279,112 @@ __device__ __forceinline__ float fp_term(float x, float wk, const FastDiv &d) {
     return (d.fast && in_fast_range(tn)) ? markstein(tn, d.b, d.y) : tn / d.b;
 }
 
-__device__ __forceinline__ void f32_tile(const dls_qtile &t, const float *__restrict__ F,
-                                         int64_t ldf, const int32_t *__restrict__ rows,
-                                         const float *__restrict__ w, int K, const FastDiv &d,
-                                         float *__restrict__ out, int e0) {
-    f32x4 acc[4];
+__device__ __forceinline__ void f32_chunk(float (&acc)[16], const float *__restrict__ Ft,
+                                          int64_t ldf, const int32_t *__restrict__ rows,
+                                          const float *__restrict__ w, int K, const FastDiv &d) {
     for (int k = 0; k < K; ++k) {
-        const f32x4 *src = reinterpret_cast<const f32x4 *>(F + (int64_t)rows[k] * ldf + t.src + e0);
+        const f32x4 *src = reinterpret_cast<const f32x4 *>(Ft + (int64_t)rows[k] * ldf);
         const float wk = w[k];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const f32x4 x = src[v];
-            f32x4 q;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) q[c] = fp_term(x[c], wk, d);
-            acc[v] = (k == 0) ? q : acc[v] + q;
+            for (int c = 0; c < 4; ++c) acc[4 * v + c] += fp_term(x[c], wk, d);
         }
     }
-    if (e0 + 16 > t.len) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[v][c] = (e0 + 4 * v + c < t.len) ? acc[v][c] : 0.f;
-    }
-    f32x4 *o = reinterpret_cast<f32x4 *>(out + t.dst + e0);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) o[v] = acc[v];
 }
 
-__global__ __launch_bounds__(kBlock) void k_dequant_fedavg(
-    const dls_qtile *__restrict__ tiles, const uint8_t *__restrict__ Q, int64_t ldq,
+// Tiles are wave tiles: <= 1024 elements of one tensor, a lane owns 16
+// consecutive elements; wave w of block b takes tile 4b + w.  The host sorts
+// the table so that the first `nfast` tiles are int tiles inside ONE channel
+// (the bulk of every large-row weight): k_dequant_fast runs only that path,
+// so its register budget is not set by the rare paths of k_dequant_general.
+// -0 + t == t for every fp32 t, so every accumulator starts at -0 and the
+// first client "is assigned" (servers/fed_server.py:62-65).
+struct WaveTile {
+    dls_qtile t;
+    int lenpad, e0, ec;
+    bool active;
+};
+
+__device__ __forceinline__ bool wave_tile(const dls_qtile *__restrict__ tiles, int ntiles,
+                                          WaveTile &wt) {
+    const int idx = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (idx >= ntiles) return false;  // wave-uniform
+    wt.t = tiles[idx];
+    wt.lenpad = (wt.t.len + 63) & ~63;  // chunks up to the 64-element row padding
+    wt.e0 = 16 * __lane_id();
+    wt.active = wt.e0 < wt.lenpad;
+    wt.ec = wt.active ? wt.e0 : wt.lenpad - 16;  // idle lanes load a valid duplicate
+    return true;
+}
+
+__device__ __forceinline__ void store16(const WaveTile &wt, float (&acc)[16],
+                                        float *__restrict__ out) {
+    if (!wt.active) return;
+    if (wt.e0 + 16 > wt.t.len) {  // tensor tail: keep the row padding zero
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = (wt.e0 + e < wt.t.len) ? acc[e] : 0.f;
+    }
+    f32x4 *o = reinterpret_cast<f32x4 *>(out + wt.t.dst + wt.e0);
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+        o[v] = f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequant_fast(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
+    const f32x2 *__restrict__ sz, int64_t ldc, const int32_t *__restrict__ rows,
+    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    float acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = -0.f;
+    const uint8_t *Qt = Q + wt.t.src + wt.ec;
+    if (wt.t.kind == 1)
+        int_one_channel<true>(acc, Qt, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+    else
+        int_one_channel<false>(acc, Qt, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+    store16(wt, acc, out);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequant_general(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const float *__restrict__ F, int64_t ldf, const f32x2 *__restrict__ sz, int64_t ldc,
     const int32_t *__restrict__ rows, const float *__restrict__ w, int K, FastDiv d,
     float *__restrict__ out) {
-    const dls_qtile t = tiles[blockIdx.x];
-    const int e0 = 16 * threadIdx.x;
-    if (e0 >= ((t.len + 63) & ~63)) return;  // chunks up to the 64-element row padding
-    if (t.kind == 1)
-        int_tile<true>(t, Q, ldq, sz, ldc, rows, w, K, d, out, e0);
-    else if (t.kind == 2)
-        int_tile<false>(t, Q, ldq, sz, ldc, rows, w, K, d, out, e0);
-    else
-        f32_tile(t, F, ldf, rows, w, K, d, out, e0);
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    const dls_qtile &t = wt.t;
+    float acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = -0.f;
+    if (t.kind == 0) {
+        f32_chunk(acc, F + t.src + wt.ec, ldf, rows, w, K, d);
+    } else {
+        const bool sgn = t.kind == 1;
+        const uint8_t *Qt = Q + t.src + wt.ec;
+        const int p = t.row_pos + wt.ec;
+        const int c = t.chan0 + p / t.row_len;
+        if (t.row_len >= 16) {
+            const int split = t.row_len - p % t.row_len;  // [0, split) in c, rest in c + 1
+            if (sgn)
+                int_lane_channels<true>(acc, Qt, ldq, sz + c, ldc, split, rows, w, K, d);
+            else
+                int_lane_channels<false>(acc, Qt, ldq, sz + c, ldc, split, rows, w, K, d);
+        } else {
+            const int r = p % t.row_len;
+            int cj[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) cj[e] = min(c + (r + e) / t.row_len, t.chan_end - 1);
+            if (sgn)
+                int_tiny_rows<true>(acc, Qt, ldq, sz, ldc, cj, rows, w, K, d);
+            else
+                int_tiny_rows<false>(acc, Qt, ldq, sz, ldc, cj, rows, w, K, d);
+        }
+    }
+    store16(wt, acc, out);
 }
 
 // ------------------------------------------------------------- min / max
@@ -402,20 +560,31 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const float *__restrict__ x
 
 using namespace dls;
 
-extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const void *Q,
-                                  int64_t ldq, const float *F, int64_t ldf, const float *sz,
-                                  int64_t ldc, const int32_t *rows, const float *weight, int32_t K,
-                                  float total, float *out, dls_stream_t stream) {
+extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_t nfast,
+                                  const void *Q, int64_t ldq, const float *F, int64_t ldf,
+                                  const float *sz, int64_t ldc, const int32_t *rows,
+                                  const float *weight, int32_t K, float total, float *out,
+                                  dls_stream_t stream) {
     DLS_REQUIRE(tiles && rows && weight && out && sz, DLS_EINVAL,
                 "dls_dequant_fedavg: null pointer");
-    DLS_REQUIRE(ntiles > 0 && K > 0, DLS_EINVAL, "dls_dequant_fedavg: ntiles=%d K=%d", ntiles, K);
+    DLS_REQUIRE(ntiles > 0 && K > 0 && nfast >= 0 && nfast <= ntiles, DLS_EINVAL,
+                "dls_dequant_fedavg: ntiles=%d nfast=%d K=%d", ntiles, nfast, K);
     DLS_REQUIRE(ldq % 16 == 0 && ldf % 4 == 0 && aligned16(out) && (!Q || aligned16(Q)) &&
                     (!F || aligned16(F)),
                 DLS_ELAYOUT, "dls_dequant_fedavg: ldq %% 16, ldf %% 4, 16-byte alignment");
     const FastDiv d = make_fastdiv(total);
-    hipLaunchKernelGGL(k_dequant_fedavg, dim3((unsigned)ntiles), dim3(kBlock), 0,
-                       as_stream(stream), tiles, reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
-                       reinterpret_cast<const f32x2 *>(sz), ldc, rows, weight, (int)K, d, out);
+    hipStream_t st = as_stream(stream);
+    constexpr int wpb = kBlock / 64;
+    if (nfast > 0)
+        hipLaunchKernelGGL(k_dequant_fast, dim3((unsigned)((nfast + wpb - 1) / wpb)), dim3(kBlock),
+                           0, st, tiles, (int)nfast, reinterpret_cast<const uint8_t *>(Q), ldq,
+                           reinterpret_cast<const f32x2 *>(sz), ldc, rows, weight, (int)K, d, out);
+    const int ngen = ntiles - nfast;
+    if (ngen > 0)
+        hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
+                           dim3(kBlock), 0, st, tiles + nfast, ngen,
+                           reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
+                           reinterpret_cast<const f32x2 *>(sz), ldc, rows, weight, (int)K, d, out);
     return check_launch("dls_dequant_fedavg");
 }
 

@@ -128,15 +128,9 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
 template <int MT, bool BETA, int kDepth>
 unsigned grid_blocks(int64_t ntiles, size_t lds) {
     // exactly the resident blocks (persistent): every wave gets ntiles/(blocks*4) tiles
-    int slot = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&slot, k_subset_gemm<MT, BETA, kDepth>, kBlock, lds) !=
-            hipSuccess || slot < 1)
-        slot = 1;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t cap =
+        resident_blocks(reinterpret_cast<const void *>(k_subset_gemm<MT, BETA, kDepth>), kBlock, lds);
     const int64_t want = (ntiles + kWaves - 1) / kWaves;
-    const int64_t cap = (int64_t)slot * cus;
     return (unsigned)(want < cap ? want : cap);
 }
 

@@ -7,11 +7,15 @@ client's fp32 dequantized tensors; here the int payloads stay int in HBM and
 one fused kernel (``dls_dequant_fedavg``) dequantizes and averages them.
 
 HBM layout per client row:
-  Q  uint8 [capacity, ldq]   int tensors' raw bytes (int8 or uint8), 64-B aligned
+  Q  uint8 [capacity, ldq]   int tensors' raw bytes (int8 or uint8); every tensor and
+                             the row pitch ldq on 256-B boundaries, so a wavefront's
+                             1 KiB load per client covers exactly 8 cache lines
   F  fp32  [capacity, ldf]   fp32 tensors (biases ...), 64-element aligned
   sz fp32  [capacity, C+1, 2] per output channel (fl32(scale), zero_point)
-and a tile table (``dls_qtile``) built once per layout: tiles of <= 4096
-elements inside one tensor, which also carry the channel bookkeeping.
+and a tile table (``dls_qtile``) built once per layout: wave tiles of <= 1024
+elements inside one tensor, which also carry the channel bookkeeping; the
+tiles whose elements all lie in one output channel come first (``nfast``) and
+run on the streamlined kernel.
 """
 import numpy as np
 import torch
@@ -19,7 +23,8 @@ import torch
 from . import _native
 from .layout import ALIGN, ParameterLayout, _round_up
 
-TILE = 4096
+TILE = 1024  # one wavefront: 64 lanes x 16 elements
+QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
 
 QTILE_DTYPE = np.dtype([("dst", "<i8"), ("src", "<i8"), ("len", "<i4"), ("kind", "<i4"),
                         ("chan0", "<i4"), ("row_len", "<i4"), ("row_pos", "<i4"),
@@ -58,7 +63,7 @@ class QuantLayout:
                 self.chan_base.append(c_off)
                 self.channels.append(C)
                 self.row_len.append(max(1, n // C))
-                q_off += _round_up(max(n, 1), ALIGN)
+                q_off += _round_up(max(n, 1), QALIGN)
                 c_off += C
             else:
                 shape = tuple(v.shape)
@@ -71,7 +76,7 @@ class QuantLayout:
                 f_off += _round_up(max(n, 1), ALIGN)
             items.append((name, shape))
         self.layout = ParameterLayout(items)
-        self.ldq = max(q_off, ALIGN)
+        self.ldq = max(q_off, QALIGN)
         self.ldf = max(f_off, ALIGN)
         self.C = c_off
         self.names = self.layout.names
@@ -88,6 +93,7 @@ class QuantLayout:
         return True
 
     def tiles(self):
+        """(table, nfast): wave tiles, one-channel int tiles first."""
         rows = []
         for i, kind in enumerate(self.kinds):
             n = self.layout.numels[i]
@@ -98,7 +104,13 @@ class QuantLayout:
                              self.chan_base[i] + e // rl if kind else 0, rl,
                              e % rl if kind else 0,
                              self.chan_base[i] + self.channels[i] if kind else 0))
-        return np.array(rows, dtype=QTILE_DTYPE)
+
+        def one_channel(r):
+            return r[3] != 0 and r[6] + r[2] <= r[5]  # kind int, row_pos + len <= row_len
+
+        fast = [r for r in rows if one_channel(r)]
+        rest = [r for r in rows if not one_channel(r)]
+        return np.array(fast + rest, dtype=QTILE_DTYPE), len(fast)
 
 
 class QuantizedClientStore:
@@ -111,7 +123,7 @@ class QuantizedClientStore:
         self.Q = torch.zeros((cap, ql.ldq), dtype=torch.uint8, device=self.device)
         self.F = torch.zeros((cap, ql.ldf), dtype=torch.float32, device=self.device)
         self.sz = torch.zeros((cap, ql.C + 1, 2), dtype=torch.float32, device=self.device)
-        t = ql.tiles()
+        t, self.nfast = ql.tiles()
         self.ntiles = len(t)
         self.tiles = torch.from_numpy(t.view(np.uint8).copy()).to(self.device)
         self._free = list(range(cap))[::-1]
@@ -167,8 +179,8 @@ class QuantizedClientStore:
             total = sum(int(n) for n in ns)
         rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
         w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
-        _native.dequant_fedavg(self.tiles, self.ntiles, self.Q, self.F, self.sz, rows_t, w_t,
-                               float(total), out)
+        _native.dequant_fedavg(self.tiles, self.ntiles, self.nfast, self.Q, self.F, self.sz,
+                               rows_t, w_t, float(total), out)
         return out
 
     def dequantize(self, row):

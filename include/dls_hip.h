@@ -130,12 +130,14 @@ int dls_sign_sgd_apply(float *param, const uint64_t *vote_planes, int64_t P, flo
                        float weight_decay, dls_stream_t stream);
 
 /* ----------------------------------------------------------------- quant
- * Tile of the flattened parameter space for the fused dequant-FedAvg kernel.
- * A tile lies inside one tensor; host code builds the table once per layout. */
+ * Wave tile of the flattened parameter space for the fused dequant-FedAvg
+ * kernels.  A tile lies inside one tensor; host code builds the table once per
+ * layout, with the "fast" tiles first: int tiles (kind 1/2) whose real
+ * elements all lie in channel chan0. */
 typedef struct dls_qtile {
     int64_t dst;     /* first output element (flat layout offset, multiple of 16) */
     int64_t src;     /* first element within a client row of Q (kind 1/2) or F (kind 0) */
-    int32_t len;     /* elements, <= 4096; lanes cover 16-element chunks up to the
+    int32_t len;     /* elements, <= 1024; lanes cover 16-element chunks up to the
                         next multiple of 64 (the rows are padded to 64) and write
                         0 past len, so the output's row padding is always zero */
     int32_t kind;    /* 0 = fp32 tensor, 1 = int8 per-channel, 2 = uint8 per-channel */
@@ -150,9 +152,10 @@ typedef struct dls_qtile {
  *   out[e] (+)= fl(fl(fl(fl(q - zp[c]) * scale[c]) * n_i) / N)  (int tensors)
  *   out[e] (+)= fl(fl(x * n_i) / N)                              (fp32 tensors)
  * bit-exact in client order.  Q int8/uint8 [*, ldq], F fp32 [*, ldf],
- * sz fp32 pairs [*, ldc] of (fl32(scale), zero_point) per channel. */
-int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const void *Q, int64_t ldq,
-                       const float *F, int64_t ldf, const float *sz, int64_t ldc,
+ * sz fp32 pairs [*, ldc] of (fl32(scale), zero_point) per channel.  Tiles
+ * [0, nfast) must be one-channel int tiles (see dls_qtile). */
+int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_t nfast, const void *Q,
+                       int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t ldc,
                        const int32_t *rows, const float *weight, int32_t K, float total,
                        float *out, dls_stream_t stream);
 

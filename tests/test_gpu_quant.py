@@ -168,3 +168,41 @@ def test_stochastic_quantize_unbiased():
     vals = set(np.unique(q.cpu().numpy()).tolist())
     assert vals == {1, 2}
     assert abs(float(deq.mean()) - 0.3) < 1e-3
+
+
+@pytest.mark.parametrize("K", [1, 63, 64, 65, 130])
+def test_dequant_fedavg_chunked_clients_one_channel(K):
+    """K across the kernels' 64-client chunks; long channel rows (one-channel
+    tiles), int8 symmetric, uint8 with zero points for which fl(zp*s) is and is
+    not exact, and a channel whose scale forces the IEEE-division path."""
+    from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
+    g = torch.Generator().manual_seed(K)
+    C, L = 5, 2500
+    payloads, n = [], []
+    for k in range(K):
+        s8 = torch.rand(C, generator=g, dtype=torch.float64) * 1e-2 + 1e-4
+        s8[3] = 3e30  # fl(deq * n) beyond the fast-division range
+        su = torch.rand(C, generator=g, dtype=torch.float64) * 1e-3 + 1e-5
+        su[0] = 0.0078125  # power of two: fl(zp * s) exact for every zp
+        payloads.append({
+            "a": (torch.randint(-128, 128, (C, L), generator=g, dtype=torch.int8), s8,
+                  torch.zeros(C, dtype=torch.int64)),
+            "b": (torch.randint(0, 256, (C, L), generator=g, dtype=torch.uint8), su,
+                  torch.randint(0, 256, (C,), generator=g)),
+            "bias": torch.randn(C, generator=g),
+        })
+        n.append(int(torch.randint(1, 1000, (1,), generator=g)))
+    store = QuantizedClientStore(payloads[0], dev, capacity=K)
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    assert store.nfast > 0
+    order = list(torch.randperm(K, generator=g).tolist())
+    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order]))
+    layout = [("a", (C, L)), ("b", (C, L)), ("bias", (C,))]
+    clients = [{k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy())
+                for k, v in p.items()} for p in payloads]
+    ref = oquant.dequant_fedavg(clients, n, order, layout)
+    assert same_bits(flat(out, layout), ref)

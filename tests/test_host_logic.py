@@ -45,13 +45,18 @@ def test_quant_layout_tiles():
                "b": torch.zeros(5),
                "u": (torch.zeros(3, 5000, dtype=torch.uint8), torch.ones(3), torch.zeros(3))}
     ql = QuantLayout(payload)
-    t = ql.tiles()
-    assert list(t["kind"]) == [1, 0, 2, 2, 2, 2]
-    assert t["len"].max() <= 4096 and all(d % 16 == 0 for d in t["dst"])
-    # the 3x5000 tensor: tiles at element 0 and 4096 -> channel 0 pos 4096, ...
+    t, nfast = ql.tiles()
+    assert t["len"].max() <= 1024 and all(d % 16 == 0 for d in t["dst"])
+    # one-channel int tiles first: the 15 tiles of the 3x5000 "u" are one-channel
+    # except those starting at 4096 and 9216, which cross a row boundary
+    fast, rest = t[:nfast], t[nfast:]
+    assert all(r["kind"] != 0 and r["row_pos"] + r["len"] <= r["row_len"] for r in fast)
+    assert all(r["kind"] == 0 or r["row_pos"] + r["len"] > r["row_len"] for r in rest)
+    assert sorted(rest["kind"].tolist()) == [0, 1, 2, 2]
+    assert nfast == 13 and sum(int(r["len"]) for r in t) == 45 + 5 + 15000
     u = t[t["kind"] == 2]
-    assert list(u["chan0"]) == [5, 5, 6, 7] or list(u["chan0"])[0] == 5
     assert all(int(r["row_pos"]) == int(r["src"] - ql.src[2]) % 5000 for r in u)
+    assert all(int(r["chan0"]) == 5 + int(r["src"] - ql.src[2]) // 5000 for r in u)
     assert ql.matches(payload)
 
 

@@ -84,11 +84,18 @@ def setup(dev):
     ql = st.qlayout
     Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
     Pf = sum(m for m, k in zip(st.layout.numels, ql.kinds) if not k)
-    W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, ptr(st.Q), st.Q.stride(0),
+    W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, st.nfast, ptr(st.Q), st.Q.stride(0),
                                                  ptr(st.F), st.F.stride(0), ptr(st.sz),
                                                  st.sz.stride(0) // 2, ptr(rows), ptr(w), 100, tot,
                                                  ptr(qo), stream()),
                   100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+    rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
+    W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, st.nfast,
+                                                         ptr(st.Q), st.Q.stride(0),
+                                                         ptr(st.F), st.F.stride(0), ptr(st.sz),
+                                                         st.sz.stride(0) // 2, ptr(rows0), ptr(w),
+                                                         100, tot, ptr(qo), stream()),
+                          100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
     C = torch.rand((50, 50), generator=g, device=dev)
     C = C / C.sum(1, keepdim=True)
     go = torch.empty((50, P), device=dev)
