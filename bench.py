@@ -191,19 +191,19 @@ def bench_sign(args, dev):
     planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
     planes[:, 1::2] &= ~planes[:, 0::2]
     sign_out = torch.empty(P, device=dev)
-    counts = torch.empty(P, dtype=torch.int32, device=dev)
+    vote = torch.empty(W, dtype=torch.int64, device=dev)
 
-    def step(a=None, b=None):
+    def step(a=None, b=None):  # the single-device server's launch (SignSGDServer)
         if a is not None:
             a.record()
-        _native.sign_vote(planes, None, K, P, sign_out, counts)
+        _native.sign_vote(planes, None, K, P, sign_out, vote_planes=vote)
         if b is not None:
             b.record()
 
     wall, kms = timed_launches(step, args.steps, args.warmup)
     ms = wall / args.steps * 1e3
     wire = W * 8
-    bytes_per_launch = K * wire + 2 * P * 4
+    bytes_per_launch = K * wire + P * 4 + wire  # client planes in, fp32 signs + packed vote out
     # worker/server pack kernel: fp32 signs -> planes, 16 clients per launch
     X = torch.sign(torch.randn((16, P), generator=g, device=dev))
     pk = torch.empty((16, W), dtype=torch.int64, device=dev)
@@ -218,7 +218,8 @@ def bench_sign(args, dev):
     _, pkms = timed_launches(pstep, args.steps, args.warmup)
     del planes, X
     return {
-        "config": "signSGD majority vote, 1000 clients x ResNet-18 (2-bit planes)",
+        "config": "signSGD majority vote, 1000 clients x ResNet-18 (2-bit planes in; fp32 "
+                  "signs + packed vote out, one launch)",
         "value": round(K * wire / (ms / 1e3) / 1e9, 2), "unit": "GB/s (packed client updates)",
         "fp32_logical_GBps": round(K * layout.numel * 4 / (ms / 1e3) / 1e9, 2),
         "ms_per_step": round(ms, 4),

@@ -54,7 +54,7 @@ SIGNATURES = {
     "dls_sign_pack_f32": ([_p, _i64, _i32, _i64, _p, _i64, _p, _p], _i32),
     "dls_sign_vote_count": ([_p, _i64, _p, _i32, _i64, _p, _p], _i32),
     "dls_sign_from_counts": ([_p, _i64, _p, _p, _p], _i32),
-    "dls_sign_vote": ([_p, _i64, _p, _i32, _i64, _p, _p, _p], _i32),
+    "dls_sign_vote": ([_p, _i64, _p, _i32, _i64, _p, _p, _p, _p], _i32),
     "dls_sign_sgd_direction": ([_p, _p, _i64, _f32, _f32, _i32, _i32, _p, _p, _p], _i32),
     "dls_sign_sgd_apply": ([_p, _p, _i64, _f32, _f32, _p], _i32),
     "dls_dequant_fedavg": ([_p, _i32, _i32, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i32, _f32, _p,
@@ -164,9 +164,11 @@ def sign_from_counts(counts, P, sign_out=None, vote_planes=None, stream=None):
                                       _stream(stream, counts)), "dls_sign_from_counts")
 
 
-def sign_vote(planes, rows, K, P, sign_out, counts=None, stream=None):
+def sign_vote(planes, rows, K, P, sign_out, counts=None, vote_planes=None, stream=None):
+    """Fused vote (dls_sign_vote): any of fp32 signs, int32 counts, packed vote."""
     _check(lib().dls_sign_vote(_ptr(planes), planes.stride(0), _ptr(rows), K, P, _ptr(counts),
-                               _ptr(sign_out), _stream(stream, planes)), "dls_sign_vote")
+                               _ptr(sign_out), _ptr(vote_planes), _stream(stream, planes)),
+           "dls_sign_vote")
     return sign_out
 
 

@@ -129,71 +129,55 @@ struct HSCounter {
     }
 };
 
-// One lane owns one group of 64 parameters (one 16-byte [pos, neg] load per
-// client, two batches of 8 clients in flight).  Outputs: counts (int32, optional) and/or
-// fp32 signs.  Exact: the counters hold K < 8 * 2^CB.
-// 64-thread blocks: one wave per block, so ~P/64/64 waves spread evenly over
-// the 256 CUs (256-thread blocks left 3-vs-2 blocks per CU, a 12% tail).
-#ifndef DLS_VOTE_BLOCK
-#define DLS_VOTE_BLOCK 64
-#endif
-#ifndef DLS_VOTE_DB
-#define DLS_VOTE_DB 1
-#endif
-constexpr int kVoteBlock = DLS_VOTE_BLOCK;
+// Vote kernel: one wave per block, lane g owns group g (64 parameters) and
+// walks all K clients: one 16-byte [pos, neg] load per client, batches of 8
+// clients double-buffered through the carry-save counters.  The grid is one
+// generation of resident waves sweeping the client rows in step.  Epilogue:
+// the counters are already bit-sliced (bit b of parameter j's count = bit j
+// of word b), so the fp32 sign needs no unpacking: a bit-sliced comparison of
+// the pos / neg counters gives two words (gt, lt) per group.  Those words (or,
+// when the int32 counts are wanted, the 2B counter words) go through LDS and
+// the wave writes its 4096 outputs coalesced, a 16-lane group per 64-parameter
+// group, instead of 64 lanes each scattering 256 bytes.
+constexpr int kVoteBlock = 64;
 
 template <int CB>
-__global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
-                                                      int64_t ldp, const int32_t *__restrict__ rows,
-                                                      int K, int64_t P, int64_t ngroups,
-                                                      int32_t *__restrict__ counts,
-                                                      float *__restrict__ sign_out) {
-    const int64_t g = (int64_t)blockIdx.x * kVoteBlock + threadIdx.x;
-    if (g >= ngroups) return;
-    HSCounter<CB> cp, cn;
-    uint64_t nan = 0;
+__device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes, int64_t ldp,
+                                            const int32_t *__restrict__ rows, int K, int64_t g,
+                                            HSCounter<CB> &cp, HSCounter<CB> &cn, uint64_t &nan) {
     const u64x2 *base = reinterpret_cast<const u64x2 *>(planes) + g;
     const int64_t ldp2 = ldp / 2;
-    // Batches of 8 clients, double-buffered: batch b+1's 8 loads are in flight
-    // while batch b runs through the carry-save adders (the vote is latency-bound
-    // at a few waves per SIMD otherwise).
     constexpr int B8 = 8;
-    auto load8 = [&](int j, u64x2 (&w)[B8]) {
+    auto load8 = [&](int j, u64x2 (&w8)[B8]) {
         if (j + B8 <= K) {
 #pragma unroll
             for (int u = 0; u < B8; ++u) {
                 const int64_t r = rows ? rows[j + u] : (j + u);
-                w[u] = __builtin_nontemporal_load(base + r * ldp2);
+                w8[u] = __builtin_nontemporal_load(base + r * ldp2);
             }
         } else {  // tail: missing clients count as zero planes
 #pragma unroll
             for (int u = 0; u < B8; ++u) {
-                w[u] = u64x2{0, 0};
+                w8[u] = u64x2{0, 0};
                 if (j + u < K) {
                     const int64_t r = rows ? rows[j + u] : (j + u);
-                    w[u] = base[r * ldp2];
+                    w8[u] = __builtin_nontemporal_load(base + r * ldp2);
                 }
             }
         }
     };
-    auto consume8 = [&](const u64x2 (&w)[B8]) {
+    auto consume8 = [&](const u64x2 (&w8)[B8]) {
         uint64_t xp[B8], xn[B8];
 #pragma unroll
         for (int u = 0; u < B8; ++u) {
-            xp[u] = w[u][0];
-            xn[u] = w[u][1];
+            xp[u] = w8[u][0];
+            xn[u] = w8[u][1];
             nan |= xp[u] & xn[u];
         }
         cp.add8(xp);
         cn.add8(xn);
     };
     u64x2 wa[B8], wb[B8];
-    if (!DLS_VOTE_DB) {
-        for (int j = 0; j < K; j += B8) {
-            load8(j, wa);
-            consume8(wa);
-        }
-    } else {
     load8(0, wa);
     for (int j = 0; j < K; j += 2 * B8) {
         if (j + B8 < K) load8(j + B8, wb);
@@ -202,35 +186,108 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
         if (j + 2 * B8 < K) load8(j + 2 * B8, wa);
         consume8(wb);
     }
-    }
-    const int64_t e0 = g * 64;
-    const bool full = e0 + 64 <= P;
-#pragma unroll 4
-    for (int q = 0; q < 16; ++q) {
-        int32_t c4[4];
-        f32x4 s4;
+}
+
+// Bit-sliced B-bit counter from the carry-save form: ones / twos / fours have
+// weights 1, 2, 4 and the CB-bit counter counts eights.
+template <int CB>
+__device__ __forceinline__ void sliced(const HSCounter<CB> &h, uint64_t (&x)[CB + 3]) {
+    x[0] = h.ones;
+    x[1] = h.twos;
+    x[2] = h.fours;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int jbit = 4 * q + t;
-            int c = cp.count(jbit) - cn.count(jbit);
-            const bool poisoned = (nan >> jbit) & 1u;
-            if (poisoned) c += DLS_SIGN_NAN_MARK;
-            c4[t] = c;
-            s4[t] = poisoned ? 0.f : (c > 0 ? 1.f : (c < 0 ? -1.f : 0.f));
+    for (int b = 0; b < CB; ++b) x[3 + b] = h.c[b];
+}
+
+template <int CB, bool COUNTS>
+__global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
+                                                          int64_t ldp,
+                                                          const int32_t *__restrict__ rows, int K,
+                                                          int64_t P, int64_t ngroups,
+                                                          int32_t *__restrict__ counts,
+                                                          float *__restrict__ sign_out,
+                                                          uint64_t *__restrict__ vote_planes,
+                                                          int64_t vote_groups) {
+    constexpr int B = CB + 3;
+    constexpr int NW = COUNTS ? 2 * B + 1 : 3;  // words per group through LDS
+    __shared__ uint64_t xw[NW][64];
+    const int lane = __lane_id();
+    const int64_t g0 = (int64_t)blockIdx.x * 64;
+    const int64_t g = g0 + lane;
+    HSCounter<CB> cp, cn;
+    uint64_t nan = 0;
+    if (g < ngroups) wave_counts<CB>(planes, ldp, rows, K, g, cp, cn, nan);
+    uint64_t xp[B], xn[B];
+    sliced<CB>(cp, xp);
+    sliced<CB>(cn, xn);
+    // bit-sliced compare, MSB first: gt = pos > neg, lt = pos < neg
+    uint64_t gt = 0, lt = 0, eq = ~0ull;
+#pragma unroll
+    for (int b = B - 1; b >= 0; --b) {
+        gt |= eq & xp[b] & ~xn[b];
+        lt |= eq & ~xp[b] & xn[b];
+        eq &= ~(xp[b] ^ xn[b]);
+    }
+    // the vote in the wire format (16 coalesced bytes per lane); NaN-poisoned
+    // and tied parameters vote 0 (neither bit)
+    if (vote_planes && g < vote_groups)
+        reinterpret_cast<u64x2 *>(vote_planes)[g] = u64x2{gt & ~nan, lt & ~nan};
+    if (COUNTS) {
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            xw[b][lane] = xp[b];
+            xw[B + b][lane] = xn[b];
         }
-        const int64_t e = e0 + 4 * q;
-        if (full) {
-            if (counts)
-                *reinterpret_cast<int4 *>(counts + e) = make_int4(c4[0], c4[1], c4[2], c4[3]);
-            if (sign_out) *reinterpret_cast<f32x4 *>(sign_out + e) = s4;
-        } else {
-            for (int t = 0; t < 4; ++t) {
-                if (e + t < P) {
-                    if (counts) counts[e + t] = c4[t];
-                    if (sign_out) sign_out[e + t] = s4[t];
+        xw[NW - 1][lane] = nan;
+    } else {
+        xw[0][lane] = gt;
+        xw[1][lane] = lt;
+        xw[2][lane] = nan;
+    }
+    if (!sign_out && !COUNTS) return;  // wave-uniform: the packed vote was all
+    __syncthreads();
+    // a 16-lane group writes one group's 64 parameters, 4 per lane
+    const int jb = 4 * (lane & 15);
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int gl = it * 4 + (lane >> 4);
+        const int64_t e = (g0 + gl) * 64 + jb;
+        if (e >= P) continue;  // P % 4 == 0: all four or none
+        f32x4 s4;
+        if (COUNTS) {
+            int pc[4] = {0, 0, 0, 0}, nc[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint32_t pw = (uint32_t)(xw[b][gl] >> jb);
+                const uint32_t nw = (uint32_t)(xw[B + b][gl] >> jb);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    pc[t] |= (int)((pw >> t) & 1u) << b;
+                    nc[t] |= (int)((nw >> t) & 1u) << b;
                 }
             }
+            const uint32_t nn = (uint32_t)(xw[NW - 1][gl] >> jb);
+            int32_t c4[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const bool poisoned = (nn >> t) & 1u;
+                const int c = pc[t] - nc[t];
+                c4[t] = poisoned ? c + DLS_SIGN_NAN_MARK : c;
+                s4[t] = poisoned ? 0.f : (c > 0 ? 1.f : (c < 0 ? -1.f : 0.f));
+            }
+            *reinterpret_cast<int4 *>(counts + e) = make_int4(c4[0], c4[1], c4[2], c4[3]);
+            if (!sign_out) continue;
+        } else {
+            const uint32_t gt = (uint32_t)(xw[0][gl] >> jb);
+            const uint32_t lt = (uint32_t)(xw[1][gl] >> jb);
+            const uint32_t nn = (uint32_t)(xw[2][gl] >> jb);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t m = 1u << t;
+                s4[t] = (nn & m) ? 0.f : ((gt & m) ? 1.f : ((lt & m) ? -1.f : 0.f));
+            }
         }
+        if (sign_out) *reinterpret_cast<f32x4 *>(sign_out + e) = s4;
     }
 }
 
@@ -341,24 +398,29 @@ __global__ __launch_bounds__(kBlock) void k_sign_sgd_apply(float *__restrict__ p
 
 template <int CB>
 int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K, int64_t P,
-                int32_t *counts, float *sign_out, hipStream_t st) {
+                int32_t *counts, float *sign_out, uint64_t *vote_planes, hipStream_t st) {
     const int64_t ngroups = (P + 63) / 64;
-    const dim3 grid((unsigned)((ngroups + kVoteBlock - 1) / kVoteBlock));
-    hipLaunchKernelGGL((k_sign_vote<CB>), grid, dim3(kVoteBlock), 0, st, planes, ldp, rows, K, P,
-                       ngroups, counts, sign_out);
+    const int64_t vote_groups = DLS_SIGN_WORDS(P) / 2;  // whole 256-parameter tiles
+    const dim3 grid((unsigned)((vote_groups + 63) / 64));
+    if (counts)
+        hipLaunchKernelGGL((k_sign_vote<CB, true>), grid, dim3(kVoteBlock), 0, st, planes, ldp,
+                           rows, K, P, ngroups, counts, sign_out, vote_planes, vote_groups);
+    else
+        hipLaunchKernelGGL((k_sign_vote<CB, false>), grid, dim3(kVoteBlock), 0, st, planes, ldp,
+                           rows, K, P, ngroups, counts, sign_out, vote_planes, vote_groups);
     return check_launch("dls_sign_vote");
 }
 
 int vote_dispatch(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K, int64_t P,
-                  int32_t *counts, float *sign_out, hipStream_t st) {
+                  int32_t *counts, float *sign_out, uint64_t *vote_planes, hipStream_t st) {
     // counts reach 8*c + 7 with c <= ceil(K/8) < 2^CB (fewer bits = fewer ops/registers)
     const int64_t c_max = (K + 7) / 8;
-    if (c_max < (1 << 2)) return launch_vote<2>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (c_max < (1 << 4)) return launch_vote<4>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (c_max < (1 << 6)) return launch_vote<6>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (c_max < (1 << 8)) return launch_vote<8>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (c_max < (1 << 12)) return launch_vote<12>(planes, ldp, rows, K, P, counts, sign_out, st);
-    if (K < (1 << 20)) return launch_vote<16>(planes, ldp, rows, K, P, counts, sign_out, st);
+    if (c_max < (1 << 2)) return launch_vote<2>(planes, ldp, rows, K, P, counts, sign_out, vote_planes, st);
+    if (c_max < (1 << 4)) return launch_vote<4>(planes, ldp, rows, K, P, counts, sign_out, vote_planes, st);
+    if (c_max < (1 << 6)) return launch_vote<6>(planes, ldp, rows, K, P, counts, sign_out, vote_planes, st);
+    if (c_max < (1 << 8)) return launch_vote<8>(planes, ldp, rows, K, P, counts, sign_out, vote_planes, st);
+    if (c_max < (1 << 12)) return launch_vote<12>(planes, ldp, rows, K, P, counts, sign_out, vote_planes, st);
+    if (K < (1 << 20)) return launch_vote<16>(planes, ldp, rows, K, P, counts, sign_out, vote_planes, st);
     set_error("dls_sign_vote: K=%d exceeds 2^20-1 clients", K);
     return DLS_EINVAL;
 }
@@ -393,18 +455,22 @@ extern "C" int dls_sign_vote_count(const uint64_t *planes, int64_t ldp, const in
                     aligned16(counts),
                 DLS_ELAYOUT, "dls_sign_vote_count: layout (ldp=%lld, P=%lld)", (long long)ldp,
                 (long long)P);
-    return vote_dispatch(planes, ldp, rows, K, P, counts, nullptr, as_stream(stream));
+    return vote_dispatch(planes, ldp, rows, K, P, counts, nullptr, nullptr, as_stream(stream));
 }
 
 extern "C" int dls_sign_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K,
-                             int64_t P, int32_t *counts, float *sign_out, dls_stream_t stream) {
-    DLS_REQUIRE(planes && sign_out, DLS_EINVAL, "dls_sign_vote: null pointer");
+                             int64_t P, int32_t *counts, float *sign_out, uint64_t *vote_planes,
+                             dls_stream_t stream) {
+    DLS_REQUIRE(planes && (sign_out || vote_planes || counts), DLS_EINVAL,
+                "dls_sign_vote: null pointer");
     DLS_REQUIRE(K > 0 && P > 0, DLS_EINVAL, "dls_sign_vote: K=%d P=%lld", K, (long long)P);
     DLS_REQUIRE(ldp >= DLS_SIGN_WORDS(P) && ldp % 2 == 0 && aligned16(planes) && P % 4 == 0 &&
-                    aligned16(sign_out) && (!counts || aligned16(counts)),
+                    (!sign_out || aligned16(sign_out)) && (!counts || aligned16(counts)) &&
+                    (!vote_planes || aligned16(vote_planes)),
                 DLS_ELAYOUT, "dls_sign_vote: layout (ldp=%lld, P=%lld)", (long long)ldp,
                 (long long)P);
-    return vote_dispatch(planes, ldp, rows, K, P, counts, sign_out, as_stream(stream));
+    return vote_dispatch(planes, ldp, rows, K, P, counts, sign_out, vote_planes,
+                         as_stream(stream));
 }
 
 extern "C" int dls_sign_from_counts(const int32_t *counts, int64_t P, float *sign_out,

@@ -84,13 +84,13 @@ class SignSGDServer(Server):
                              "reference's fp32 sum would not be a majority vote")
         P = self._layout.P
         sign_out = torch.empty(P, dtype=torch.float32, device=self.device)
-        counts = torch.empty(P, dtype=torch.int32, device=self.device)
-        _native.sign_vote(self._planes, None, self.worker_number, P, sign_out, counts)
         vote_planes = torch.empty(_native.sign_words(P), dtype=torch.int64, device=self.device)
-        _native.sign_from_counts(counts, P, None, vote_planes)
+        # one launch: fp32 signs for the reference's broadcast list and the packed
+        # vote for device-side workers (no int32 counts on a single device)
+        _native.sign_vote(self._planes, None, self.worker_number, P, sign_out,
+                          vote_planes=vote_planes)
         result = SignVoteResult(self._layout.views(sign_out).values())
         result.vote_planes = vote_planes
-        result.counts = counts
         self.sign_gradients = []
         return RepeatedResult(data=result, num=self.worker_number)
 

@@ -111,9 +111,11 @@ int dls_sign_vote_count(const uint64_t *planes, int64_t ldp, const int32_t *rows
 int dls_sign_from_counts(const int32_t *counts, int64_t P, float *sign_out,
                          uint64_t *vote_planes, dls_stream_t stream);
 
-/* Fused single-device vote: planes -> fp32 signs (counts optional, may be NULL). */
-int dls_sign_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K,
-                  int64_t P, int32_t *counts, float *sign_out, dls_stream_t stream);
+/* Fused single-device vote: planes -> any of fp32 signs, int32 counts and the
+ * vote packed in the plane format (DLS_SIGN_WORDS(P) words, NaN-poisoned and
+ * tied parameters 0); NULL outputs are skipped, at least one must be given. */
+int dls_sign_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int32_t K, int64_t P,
+                  int32_t *counts, float *sign_out, uint64_t *vote_planes, dls_stream_t stream);
 
 /* Worker step, workers/sign_sgd_worker.py:32-44 fused: momentum / dampening /
  * nesterov on grad (buf updated in place; first=1 clones), torch.sign, pack to

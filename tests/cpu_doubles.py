@@ -78,12 +78,12 @@ def sign_from_counts(counts, P, sign_out=None, vote_planes=None, stream=None):
         vote_planes[: row.size].copy_(torch.from_numpy(row.view(np.int64)))
 
 
-def sign_vote(planes, rows, K, P, sign_out, counts=None, stream=None):
+def sign_vote(planes, rows, K, P, sign_out, counts=None, vote_planes=None, stream=None):
     c = torch.empty(P, dtype=torch.int32)
     sign_vote_count(planes, rows, K, P, c)
     if counts is not None:
         counts.copy_(c)
-    sign_from_counts(c, P, sign_out)
+    sign_from_counts(c, P, sign_out, vote_planes)
     return sign_out
 
 

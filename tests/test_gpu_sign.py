@@ -172,3 +172,31 @@ def test_sign_worker_golden_bit_exact():
                 newp[sl] = pd.cpu()
             p = newp
             assert same_bits(p.numpy(), z[f"{k}_s{s}_param"]), (k, s)
+
+
+@pytest.mark.parametrize("P,K", [(4, 3), (1000, 17), (4096 + 68, 64), (70000, 130)])
+def test_fused_vote_planes_match_two_stage(P, K):
+    """dls_sign_vote's packed vote (and sign-only mode) == counts -> sign_from_counts."""
+    from distributed_learning_simulator_amd import _native
+    g = np.random.default_rng(P + K)
+    S = np.sign(g.standard_normal((K, P))).astype(np.float32)
+    S[:, ::7] = 0
+    S[K // 2, 3] = np.nan  # one poisoned parameter
+    S[:, 1] = 0  # a tie at zero
+    planes, _ = pack(S)
+    Pp = (P + 3) // 4 * 4
+    Wd = _native.sign_words(Pp)
+    s1 = torch.empty(Pp, device=dev)
+    v1 = torch.full((Wd,), 0x55, dtype=torch.int64, device=dev)
+    _native.sign_vote(planes, None, K, Pp, s1, vote_planes=v1)
+    c = torch.empty(Pp, dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, None, K, Pp, c)
+    s2 = torch.empty(Pp, device=dev)
+    v2 = torch.zeros(Wd, dtype=torch.int64, device=dev)
+    _native.sign_from_counts(c, Pp, s2, v2)
+    assert same_bits(s1.cpu().numpy(), s2.cpu().numpy())
+    assert torch.equal(v1, v2)
+    assert same_bits(s1.cpu().numpy()[:P], osign.majority_vote(S))
+    v3 = torch.zeros(Wd, dtype=torch.int64, device=dev)  # packed vote alone
+    _native.sign_vote(planes, None, K, Pp, None, vote_planes=v3)
+    assert torch.equal(v3, v2)

@@ -62,7 +62,10 @@ def setup(dev):
     so = torch.empty(P, device=dev)
     cnt = torch.empty(P, dtype=torch.int32, device=dev)
     W["vote"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, ptr(cnt), ptr(so),
-                                           stream()), 1000 * Wd * 8 + 2 * P * 4)
+                                           None, stream()), 1000 * Wd * 8 + 2 * P * 4)
+    vp = torch.empty(Wd, dtype=torch.int64, device=dev)
+    W["vote_sign"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, None, ptr(so),
+                                                ptr(vp), stream()), 1000 * Wd * 8 + P * 4 + Wd * 8)
     X = torch.sign(torch.randn((16, P), generator=g, device=dev))
     pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
     W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
