@@ -27,7 +27,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kTileP = 128;
+#ifndef DLS_GEMM_NT
+#define DLS_GEMM_NT 4  // N-tiles (32 columns each) per wave: 16-byte (4) or 8-byte (2) loads
+#endif
+constexpr int kNT = DLS_GEMM_NT;
+constexpr int kTileP = 32 * kNT;
+typedef float f32xnt __attribute__((ext_vector_type(kNT)));
 constexpr int kMaxK = 256;
 
 template <int MT, bool BETA, int kDepth>
@@ -58,26 +63,26 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
     // One flattened (tile, k-step) stream: the U loads of the next 4 k-steps are
     // in flight while the MFMAs of the current one run, and across a tile seam
     // they already fetch the next tile, so the epilogue stores overlap them.
-    auto loadB = [&](int64_t t, int s) -> f32x4 {
-        const int64_t pp = t * kTileP + 4 * col;
+    auto loadB = [&](int64_t t, int s) -> f32xnt {
+        const int64_t pp = t * kTileP + kNT * col;
         const int32_t r = srow[2 * s + h];
-        f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (r >= 0 && t < ntiles && pp + 4 <= P)
-            b = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + pp));
+        f32xnt b = f32xnt(0.f);
+        if (r >= 0 && t < ntiles && pp + kNT <= P)
+            b = __builtin_nontemporal_load(reinterpret_cast<const f32xnt *>(U + (int64_t)r * ldu + pp));
         return b;
     };
-    f32x4 b[kDepth];
+    f32xnt b[kDepth];
 #pragma unroll
     for (int i = 0; i < kDepth; ++i) b[i] = loadB(tile, i);
     for (; tile < ntiles; tile += stride) {
-        const int64_t p = tile * kTileP + 4 * col;  // this lane's 4 parameters
-        const bool inb = p + 4 <= P;
+        const int64_t p = tile * kTileP + kNT * col;  // this lane's kNT parameters
+        const bool inb = p + kNT <= P;
         const int64_t next = tile + stride;
-        f32x16 acc[MT][4];
+        f32x16 acc[MT][kNT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
-            for (int n = 0; n < 4; ++n) {
+            for (int n = 0; n < kNT; ++n) {
                 if (BETA && inb) {
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
@@ -90,13 +95,13 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
                 }
             }
         }
-        auto mma = [&](int s, const f32x4 &b) {
+        auto mma = [&](int s, const f32xnt &b) {
             const int k = 2 * s + h;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const float a = Ct[k * 32 * MT + 32 * mt + col];
 #pragma unroll
-                for (int n = 0; n < 4; ++n)
+                for (int n = 0; n < kNT; ++n)
                     acc[mt][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[n], acc[mt][n], 0, 0, 0);
             }
         };
@@ -116,9 +121,15 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int row = 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (row < S)
-                        *reinterpret_cast<f32x4 *>(out + (int64_t)row * ldo + p) =
-                            f32x4{acc[mt][0][r], acc[mt][1][r], acc[mt][2][r], acc[mt][3][r]};
+                    if (row < S) {
+                        f32xnt v;
+#pragma unroll
+                        for (int n = 0; n < kNT; ++n) v[n] = acc[mt][n][r];
+                        // non-temporal: the subset models stream out past the caches
+                        // (measured 4 % faster with the U reads in flight)
+                        __builtin_nontemporal_store(
+                            v, reinterpret_cast<f32xnt *>(out + (int64_t)row * ldo + p));
+                    }
                 }
             }
         }
