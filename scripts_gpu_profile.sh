@@ -7,7 +7,7 @@
 #   4. SQ instruction / stall counters (one pass: 8 SQ + 1 GRBM)
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")" && pwd)}"
-TAG="${1:-r01}"
+TAG="${1:-r01b}"
 OUT="$ROOT/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

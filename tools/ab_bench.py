@@ -116,7 +116,9 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     libs = {os.path.basename(p)[7:-3]: load(p)
-            for p in sorted(glob.glob(os.path.join(ROOT, "tools", "_variants", "libdls_*.so")))}
+            for p in sorted(glob.glob(os.path.join(
+                os.environ.get("DLS_VARIANTS", os.path.join(ROOT, "tools", "_variants")),
+                "libdls_*.so")))}
     W = setup(dev)
     res = {}
     for wl in args.workloads.split(","):

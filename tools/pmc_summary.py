@@ -18,12 +18,13 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-WORKLOADS = {  # workload -> (kernel regex, key in pmc_traffic.json)
-    "headline": [("k_fedavg_exact", "headline")],
-    "fedavg_k1000": [("k_fedavg_exact", "fedavg_k1000")],
-    "sign_vote": [("k_sign_vote", "sign_vote"), ("k_sign_pack", "sign_pack")],
-    "fed_quant": [("k_dequant_fedavg", "fed_quant")],
-    "shapley_gemm": [("k_subset_gemm", "shapley_gemm")],
+WORKLOADS = {  # workload -> [(kernel regexes summed per launch, key in pmc_traffic.json)]
+    "headline": [(["k_fedavg_exact_pipe"], "headline")],
+    "fedavg_k1000": [(["k_fedavg_exact_pipe"], "fedavg_k1000")],
+    "sign_vote": [(["k_sign_vote"], "sign_vote"), (["k_sign_pack"], "sign_pack")],
+    # one dls_dequant_fedavg call = the one-channel kernel + the general kernel
+    "fed_quant": [(["k_dequant_fast", "k_dequant_general"], "fed_quant")],
+    "shapley_gemm": [(["k_subset_gemm"], "shapley_gemm")],
 }
 
 
@@ -31,7 +32,7 @@ def values(path, counter, kernel):
     out = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row["Counter_Name"] == counter and re.search(r"\b" + kernel + r"\b", row["Kernel_Name"]):
+            if row["Counter_Name"] == counter and re.search(r"\b" + kernel + r"(\b|<)", row["Kernel_Name"]):
                 out.append(float(row["Counter_Value"]))
     return out
 
@@ -40,24 +41,31 @@ def main(tag):
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     res, lines = {}, []
     for wl, kernels in WORKLOADS.items():
-        for kernel, key in kernels:
+        for names, key in kernels:
+            fm = wm = 0.0
+            nl = 0
+            kernel = "+".join(names)
             try:
-                f = values(os.path.join(base, f"pmc_{wl}_FETCH_SIZE", "run_counter_collection.csv"),
-                           "FETCH_SIZE", kernel)
-                w = values(os.path.join(base, f"pmc_{wl}_WRITE_SIZE", "run_counter_collection.csv"),
-                           "WRITE_SIZE", kernel)
+                for name in names:
+                    f = values(os.path.join(base, f"pmc_{wl}_FETCH_SIZE",
+                                            "run_counter_collection.csv"), "FETCH_SIZE", name)
+                    w = values(os.path.join(base, f"pmc_{wl}_WRITE_SIZE",
+                                            "run_counter_collection.csv"), "WRITE_SIZE", name)
+                    if f and w:
+                        fm += statistics.median(f)
+                        wm += statistics.median(w)
+                        nl = max(nl, len(f))
             except OSError:
                 continue
-            if not f or not w:
+            if not nl:
                 continue
-            fm, wm = statistics.median(f), statistics.median(w)
             rd, wr = 2.0 * fm * 1024.0, wm * 1024.0
             res[key] = {"kernel": kernel, "fetch_size_kib": fm, "write_size_kib": wm,
                         "hbm_read_bytes": rd, "hbm_write_bytes": wr,
-                        "hbm_bytes_per_launch": rd + wr, "launches": len(f)}
-            lines.append(f"{key:14s} {kernel:18s} FETCH_SIZE {fm:12.0f} KiB (x2 -> {rd / 1e9:8.3f} GB) "
+                        "hbm_bytes_per_launch": rd + wr, "launches": nl}
+            lines.append(f"{key:14s} {kernel:36s} FETCH_SIZE {fm:12.0f} KiB (x2 -> {rd / 1e9:8.3f} GB) "
                          f"WRITE_SIZE {wm:11.0f} KiB ({wr / 1e9:7.3f} GB) total "
-                         f"{(rd + wr) / 1e9:8.3f} GB/launch  [{len(f)} launches]")
+                         f"{(rd + wr) / 1e9:8.3f} GB/launch  [{nl} launches]")
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.txt"), "w") as fh:
