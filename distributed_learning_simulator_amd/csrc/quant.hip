@@ -251,6 +251,70 @@ __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_
     }
 }
 
+// Lanes in different channels but none straddling a channel boundary (channel
+// rows a multiple of 16 long, e.g. every 3x3 conv weight of VGG-16 / ResNet):
+// the one-channel pipeline with each lane's (scale, zero point) loaded per
+// client next to its payload (8 bytes, a handful of distinct lines per wave).
+template <bool SIGNED>
+__device__ __forceinline__ void int_lane_pipelined(float (&acc)[16], const uint8_t *__restrict__ Qt,
+                                                   int64_t ldq, const f32x2 *__restrict__ szl,
+                                                   int64_t ldc, const int32_t *__restrict__ rows,
+                                                   const float *__restrict__ w, int K,
+                                                   const FastDiv &d) {
+    constexpr int U = DLS_QUANT_U;
+    struct Batch {
+        u32x4 qv[U];
+        f32x2 sz[U];
+        float wk[U];
+    };
+    const float zadj = SIGNED ? 128.f : 0.f;
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    auto one = [&](const u32x4 qv, f32x2 sz, float wk) {
+        const float sc = sz.x, z = sz.y + zadj, zs = z * sc;
+        const bool zfma = __builtin_fmaf(z, sc, -zs) == 0.f;  // fl(z*s) exact
+        const bool fast = d.fast && scale_fast(sc * wk);
+        if (__ballot(!(zfma && fast)) == 0) {  // wave-uniform common case
+            accum16_one<true, true>(acc, qv, sc, zs, z, wk, d);
+        } else if (zfma && fast) {
+            accum16_one<true, true>(acc, qv, sc, zs, z, wk, d);
+        } else if (fast) {
+            accum16_one<false, true>(acc, qv, sc, zs, z, wk, d);
+        } else {
+            accum16_one<false, false>(acc, qv, sc, zs, z, wk, d);
+        }
+    };
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        cr.advance(rows, w, K, base);
+        auto fetch = [&](int j, u32x4 &qv, f32x2 &sz, float &wk) {
+            const int64_t r = readlane_i(tr, j);
+            qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
+            if (SIGNED) qv ^= 0x80808080u;  // int8 q read as the unsigned byte q + 128
+            sz = szl[r * ldc];
+            wk = readlane_f(tw, j);
+        };
+        chunk_pipeline<U, Batch>(
+            min(64, K - base),
+            [&](int j0, Batch &bt) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) fetch(j0 + u, bt.qv[u], bt.sz[u], bt.wk[u]);
+            },
+            [&](const Batch &bt) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) one(bt.qv[u], bt.sz[u], bt.wk[u]);
+            },
+            [&](int j) {
+                u32x4 qv;
+                f32x2 sz;
+                float wk;
+                fetch(j, qv, sz, wk);
+                one(qv, sz, wk);
+            });
+    }
+}
+
 // Channel rows shorter than 16 elements: per-element channel lookup.
 template <bool SIGNED>
 __device__ __forceinline__ void int_tiny_rows(float (&acc)[16], const uint8_t *__restrict__ Qt,
@@ -369,10 +433,16 @@ __global__ __launch_bounds__(kBlock) void k_dequant_general(
         const int c = t.chan0 + p / t.row_len;
         if (t.row_len >= 16) {
             const int split = t.row_len - p % t.row_len;  // [0, split) in c, rest in c + 1
-            if (sgn)
+            if (__ballot(split < 16) == 0) {  // wave-uniform: no lane straddles a channel
+                if (sgn)
+                    int_lane_pipelined<true>(acc, Qt, ldq, sz + c, ldc, rows, w, K, d);
+                else
+                    int_lane_pipelined<false>(acc, Qt, ldq, sz + c, ldc, rows, w, K, d);
+            } else if (sgn) {
                 int_lane_channels<true>(acc, Qt, ldq, sz + c, ldc, split, rows, w, K, d);
-            else
+            } else {
                 int_lane_channels<false>(acc, Qt, ldq, sz + c, ldc, split, rows, w, K, d);
+            }
         } else {
             const int r = p % t.row_len;
             int cj[16];
