@@ -335,7 +335,8 @@ def bench_shapley_evals(args, dev):
     g = torch.Generator().manual_seed(SEED + 6)
     coalitions = [sorted(torch.randperm(K, generator=g)[: 1 + i % K].tolist())
                   for i in range(args.evals + 2)]
-    model = ResNet18().to(dev).eval()
+    model = ResNet18().to(dev).eval().to(memory_format=torch.channels_last)
+    X = X.contiguous(memory_format=torch.channels_last)  # NHWC convs (tools/eval_probe.py)
     mu = ModelUtil(model)
     autocast = {"enabled": False}
 
@@ -348,8 +349,9 @@ def bench_shapley_evals(args, dev):
         correct = 0
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16,
                                              enabled=autocast["enabled"]):
-            for i in range(0, X.shape[0], 2500):
-                correct += int((model(X[i:i + 2500]).argmax(1) == y[i:i + 2500]).sum())
+            for i in range(0, X.shape[0], 1000):
+                correct += (model(X[i:i + 1000]).argmax(1) == y[i:i + 1000]).sum()
+        correct = int(correct)
         return correct / X.shape[0]
 
     def timed():
@@ -363,12 +365,11 @@ def bench_shapley_evals(args, dev):
 
     accs, el = timed()
     autocast["enabled"] = True
-    model.to(memory_format=torch.channels_last)
-    X = X.to(memory_format=torch.channels_last)
     accs16, el16 = timed()
     del U
     return {"config": f"Shapley utility evals: subset model + ResNet-18 inference on "
-                      f"{args.eval_images} CIFAR-10-shaped images (fp32), 50 clients",
+                      f"{args.eval_images} CIFAR-10-shaped images (fp32, NHWC, batch 1000), "
+                      f"50 clients",
             "value": round(len(accs) / el, 3), "unit": "subset-evals/s per GPU",
             "ms_per_eval": round(el / len(accs) * 1e3, 2),
             "utility_range": [round(min(accs), 4), round(max(accs), 4)],
@@ -470,7 +471,9 @@ def main():
         dist.barrier()
     if rank == 0:
         line = {
-            "metric": "client-update GB/s aggregated per FL round",
+            # BASELINE.json's metric; `value` is its first part (client-update GB/s),
+            # the second part (Shapley subset-evals/s) is `shapley_subset_evals_per_s`
+            "metric": "client-update GB/s aggregated per FL round + Shapley subset-evals/sec",
             "value": round(value, 2) if value is not None else None, "unit": "GB/s",
             "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4) if ms is not None else None,
@@ -480,7 +483,9 @@ def main():
                                    "fp32) client updates per GPU, bit-exact reference order",
                        "parallelism": f"clients sharded over {world} GPU(s) + RCCL all-reduce",
                        **extra},
-            "roofline": rf, "cpu_baseline": cpu, "components": components,
+            "roofline": rf, "cpu_baseline": cpu,
+            "shapley_subset_evals_per_s": (components.get("shapley_evals") or {}).get("value"),
+            "components": components,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -59,16 +59,24 @@ class Inferencer:
     def inference(self):
         X, y = self.dataset
         self.model.eval()
-        correct, loss_sum = 0, 0.0
+        if X.dim() == 4 and torch.device(self.device).type == "cuda":
+            # NHWC convolutions: measured 8-18 % faster than NCHW for this model family
+            # on MI355X (tools/eval_probe.py); results are the same up to fp32 reassociation
+            self.model.to(memory_format=torch.channels_last)
+        correct = torch.zeros((), dtype=torch.int64, device=self.device)
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         for i in range(0, X.shape[0], self.batch_size):
             xb = X[i:i + self.batch_size].to(self.device, non_blocking=True)
             yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
+            if xb.dim() == 4 and xb.is_cuda:
+                xb = xb.contiguous(memory_format=torch.channels_last)
             out = self.model(xb)
-            loss_sum += float(torch.nn.functional.cross_entropy(out, yb, reduction="sum"))
-            correct += int((out.argmax(1) == yb).sum())
+            loss_sum += torch.nn.functional.cross_entropy(out, yb, reduction="sum").double()
+            correct += (out.argmax(1) == yb).sum()
         n = X.shape[0]
-        self.accuracy_metric.value = correct / n
-        self.loss_metric.value = torch.tensor(loss_sum / n)
+        # one host synchronisation per evaluation instead of two per batch
+        self.accuracy_metric.value = int(correct) / n
+        self.loss_metric.value = torch.tensor(float(loss_sum) / n)
         return self.loss_metric.value, self.accuracy_metric.value, None
 
 
