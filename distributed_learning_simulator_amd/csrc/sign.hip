@@ -141,30 +141,17 @@ struct HSCounter {
 // group, instead of 64 lanes each scattering 256 bytes.
 constexpr int kVoteBlock = 64;
 
-template <int CB>
+template <int CB, bool ROWS>
 __device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes, int64_t ldp,
                                             const int32_t *__restrict__ rows, int K, int64_t g,
                                             HSCounter<CB> &cp, HSCounter<CB> &cn, uint64_t &nan) {
     const u64x2 *base = reinterpret_cast<const u64x2 *>(planes) + g;
     const int64_t ldp2 = ldp / 2;
     constexpr int B8 = 8;
+    auto row = [&](int k) -> int64_t { return ROWS ? (int64_t)rows[k] : (int64_t)k; };
     auto load8 = [&](int j, u64x2 (&w8)[B8]) {
-        if (j + B8 <= K) {
 #pragma unroll
-            for (int u = 0; u < B8; ++u) {
-                const int64_t r = rows ? rows[j + u] : (j + u);
-                w8[u] = __builtin_nontemporal_load(base + r * ldp2);
-            }
-        } else {  // tail: missing clients count as zero planes
-#pragma unroll
-            for (int u = 0; u < B8; ++u) {
-                w8[u] = u64x2{0, 0};
-                if (j + u < K) {
-                    const int64_t r = rows ? rows[j + u] : (j + u);
-                    w8[u] = __builtin_nontemporal_load(base + r * ldp2);
-                }
-            }
-        }
+        for (int u = 0; u < B8; ++u) w8[u] = __builtin_nontemporal_load(base + row(j + u) * ldp2);
     };
     auto consume8 = [&](const u64x2 (&w8)[B8]) {
         uint64_t xp[B8], xn[B8];
@@ -177,14 +164,35 @@ __device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes,
         cp.add8(xp);
         cn.add8(xn);
     };
-    u64x2 wa[B8], wb[B8];
-    load8(0, wa);
-    for (int j = 0; j < K; j += 2 * B8) {
-        if (j + B8 < K) load8(j + B8, wb);
-        consume8(wa);
-        if (j + B8 >= K) break;
-        if (j + 2 * B8 < K) load8(j + 2 * B8, wa);
-        consume8(wb);
+    // batches of 8 clients, double-buffered; loads inside the steady-state loop
+    // are unconditional so every consume waits with an exact vmcnt
+    const int nb = K / B8;
+    if (nb > 0) {
+        u64x2 wa[B8], wb[B8];
+        load8(0, wa);
+        int b = 0;
+        for (; b + 2 < nb; b += 2) {
+            load8((b + 1) * B8, wb);
+            consume8(wa);
+            load8((b + 2) * B8, wa);
+            consume8(wb);
+        }
+        if (b + 1 < nb) {
+            load8((b + 1) * B8, wb);
+            consume8(wa);
+            consume8(wb);
+        } else {
+            consume8(wa);
+        }
+    }
+    if (nb * B8 < K) {  // tail: missing clients count as zero planes
+        u64x2 w8[B8];
+#pragma unroll
+        for (int u = 0; u < B8; ++u) {
+            const int k = nb * B8 + u;
+            w8[u] = k < K ? __builtin_nontemporal_load(base + row(k) * ldp2) : u64x2{0, 0};
+        }
+        consume8(w8);
     }
 }
 
@@ -216,7 +224,12 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
     const int64_t g = g0 + lane;
     HSCounter<CB> cp, cn;
     uint64_t nan = 0;
-    if (g < ngroups) wave_counts<CB>(planes, ldp, rows, K, g, cp, cn, nan);
+    if (g < ngroups) {
+        if (rows)
+            wave_counts<CB, true>(planes, ldp, rows, K, g, cp, cn, nan);
+        else
+            wave_counts<CB, false>(planes, ldp, rows, K, g, cp, cn, nan);
+    }
     uint64_t xp[B], xn[B];
     sliced<CB>(cp, xp);
     sliced<CB>(cn, xn);
