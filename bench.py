@@ -410,7 +410,57 @@ def cpu_baseline(args):
             "kind": "port",
             "sample": f"{Kc} ResNet-18 client dicts (fp32, 62 tensors), reference torch op "
                       f"sequence, {reps} reps in {el:.1f}s",
-            "cpu_model": model or platform.processor(), "ms_per_aggregation": round(per * 1e3, 2)}
+            "cpu_model": model or platform.processor(), "ms_per_aggregation": round(per * 1e3, 2),
+            "components": cpu_components(args, threads)}
+
+
+def cpu_components(args, threads):
+    """The reference's torch op sequences for configs 3 and 4 on the host cores
+    (bounded samples; per-client rates scale linearly in K)."""
+    from oracle.fedavg import fedavg_torch_cpu  # test infrastructure, timed only
+    from oracle.quant import dequant_torch_cpu
+    from oracle.sign import sign_vote_torch_cpu
+    res = {}
+    g = torch.Generator().manual_seed(SEED + 9)
+    shapes = resnet18_cifar()
+    P = sum(math.prod(s) for _, s in shapes)
+    Ks = 20  # servers/sign_sgd_server.py:16-18 on 20 clients' fp32 sign lists
+    signs = [[torch.sign(torch.randn(s, generator=g)) for _, s in shapes] for _ in range(Ks)]
+    sign_vote_torch_cpu(signs)
+    t0, reps = time.perf_counter(), 0
+    while time.perf_counter() - t0 < args.cpu_seconds / 2 or reps < 2:
+        sign_vote_torch_cpu(signs)
+        reps += 1
+    per = (time.perf_counter() - t0) / reps
+    res["sign_vote"] = {"value": round(Ks * P * 4 / per / 1e9, 3),
+                        "unit": "GB/s (fp32 sign lists, the reference's wire format)",
+                        "cores": threads, "kind": "port",
+                        "sample": f"{Ks} clients x ResNet-18, {reps} reps",
+                        "ms_per_vote": round(per * 1e3, 2)}
+    del signs
+    # servers/fed_quant_server.py:25-33 per client + servers/fed_server.py:52-65
+    Kq = 2
+    payloads = []
+    for _ in range(Kq):
+        d = {}
+        for name, s in vgg16():
+            if len(s) >= 2:
+                d[name] = (torch.randint(-128, 128, s, generator=g, dtype=torch.int8),
+                           torch.rand(s[0], generator=g, dtype=torch.float64) * 1e-2,
+                           torch.zeros(s[0], dtype=torch.int64))
+            else:
+                d[name] = torch.randn(s, generator=g)
+        payloads.append(d)
+    Pv = sum(math.prod(s) for _, s in vgg16())
+    t0 = time.perf_counter()
+    deq = [dequant_torch_cpu(p) for p in payloads]
+    fedavg_torch_cpu(deq, [500] * Kq, list(range(Kq)))
+    el = time.perf_counter() - t0
+    res["fed_quant"] = {"value": round(Kq * Pv / el / 1e9, 3),
+                        "unit": "GB/s (int8 client updates)", "cores": threads, "kind": "port",
+                        "sample": f"{Kq} clients x VGG-16 dequant (channel loop) + FedAvg, 1 rep",
+                        "ms_per_client": round(el / Kq * 1e3, 1)}
+    return res
 
 
 def main():

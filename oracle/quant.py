@@ -91,3 +91,21 @@ def requantize_tensors(flat, layout):
         zps.append(z)
         off += m
     return q, np.array(scales, np.float32), np.array(zps, np.int32), deq
+
+
+def dequant_torch_cpu(client_parameter):
+    """The reference's own torch op sequence on the CPU
+    (servers/fed_quant_server.py:25-33): ``weight.float()`` then a Python loop over
+    the output channels ``weight[c] = (v - zero_point[c]) * scale[c]``.  Timed by
+    bench.py's CPU baseline (dequant_channel is the parity reference)."""
+    out = {}
+    for k, v in client_parameter.items():
+        if isinstance(v, tuple):
+            weight, scale, zero_point = v
+            weight = weight.float()
+            for idx, row in enumerate(weight):
+                weight[idx] = (row - zero_point[idx]) * scale[idx]
+            out[k] = weight
+        else:
+            out[k] = v
+    return out

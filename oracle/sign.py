@@ -102,3 +102,13 @@ def worker_apply(p, vote, lr, weight_decay):
     """workers/sign_sgd_worker.py:48-57: d = vote (+ wd*p); p += -lr * d."""
     from . import _c
     return _c.sign_apply(p, vote, lr, weight_decay)
+
+
+def sign_vote_torch_cpu(sign_gradients):
+    """The reference's own torch op sequence on the CPU (servers/sign_sgd_server.py:16-18):
+    per tensor a Python ``sum`` over the clients' fp32 sign tensors, then ``torch.sign``.
+    ``sign_gradients``: list (one per client) of lists of fp32 CPU tensors.  Timed by
+    bench.py's CPU baseline; not used as a parity reference (majority_vote is)."""
+    import torch
+    total = [sum(i) for i in zip(*sign_gradients)]
+    return [torch.sign(g) for g in total]
