@@ -105,7 +105,16 @@ struct ChunkRows {
 // as q ^ 0x80).  Packed fp32: every op below is a v_pk_*_f32 over two
 // elements with the scalar ops' IEEE roundings.  When fl(z*s) is exact (always
 // for symmetric int8, z = 128), fl((x - z)*s) == fma(x, s, -z*s): one op.
-template <bool ZFMA, bool FAST>
+// Byte k of a dword as fp32: the unsigned value (v_cvt_f32_ubyteK) or, for
+// int8, the sign-extended one (v_cvt_f32_i32 with an SDWA sext byte select):
+// one VALU op either way.
+template <bool SEXT>
+__device__ __forceinline__ float byte_val(uint32_t w, int k) {
+    if (SEXT) return (float)(int8_t)(w >> (8 * k));
+    return (float)((w >> (8 * k)) & 0xffu);
+}
+
+template <bool ZFMA, bool FAST, bool SEXT = false>
 __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s, float zs, float z,
                                             float wk, const FastDiv &d) {
     const f32x2 s2 = f32x2{s, s}, w2 = f32x2{wk, wk};
@@ -113,7 +122,8 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
     const f32x2 b2 = f32x2{d.b, d.b}, y2 = f32x2{d.y, d.y};
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
-        const f32x2 x = f32x2{byte_f32(qv[j >> 2], j & 3), byte_f32(qv[j >> 2], (j + 1) & 3)};
+        const f32x2 x = f32x2{byte_val<SEXT>(qv[j >> 2], j & 3),
+                              byte_val<SEXT>(qv[j >> 2], (j + 1) & 3)};
         const f32x2 deq = ZFMA ? pk_fma(x, s2, nzs) : (x - z2) * s2;
         const f32x2 t = deq * w2;
         f32x2 q;
@@ -135,11 +145,15 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
 }
 
 template <bool SIGNED>
-__device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t *__restrict__ Qt,
-                                                int64_t ldq, const f32x2 *__restrict__ szc,
-                                                int64_t ldc, const int32_t *__restrict__ rows,
+__device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t *__restrict__ Q,
+                                                uint32_t qoff, int64_t ldq,
+                                                const f32x2 *__restrict__ szc, int64_t ldc,
+                                                const int32_t *__restrict__ rows,
                                                 const float *__restrict__ w, int K,
                                                 const FastDiv &d) {
+    // int8 bytes convert sign-extended (value q, zero point zp); uint8 bytes
+    // unsigned.  The payload address is (Q + row*ldq) [wave-uniform, SALU] +
+    // qoff [this lane's 32-bit offset].
     constexpr int U = DLS_QUANT_U;
     struct Batch {
         u32x4 qv[U];
@@ -148,17 +162,16 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
     ChunkRows cr;
     cr.init(rows, w, K);
     f32x2 nsz = szc[(int64_t)cr.r0 * ldc];  // this wave's channel, client 64c + lane
-    const float zadj = SIGNED ? 128.f : 0.f;
-    auto one = [&](const u32x4 qv, float s, float z, float wk) {
-        const float zs = z * s;
-        const bool zfma = __builtin_fmaf(z, s, -zs) == 0.f;  // fl(z*s) exact
-        const bool fast = d.fast && scale_fast(s * wk);
+    auto one = [&](const u32x4 qv, float sc, float z, float wk) {
+        const float zs = z * sc;
+        const bool zfma = __builtin_fmaf(z, sc, -zs) == 0.f;  // fl(z*s) exact
+        const bool fast = d.fast && scale_fast(sc * wk);
         if (__builtin_expect(zfma && fast, 1))
-            accum16_one<true, true>(acc, qv, s, zs, z, wk, d);
+            accum16_one<true, true, SIGNED>(acc, qv, sc, zs, z, wk, d);
         else if (fast)
-            accum16_one<false, true>(acc, qv, s, zs, z, wk, d);
+            accum16_one<false, true, SIGNED>(acc, qv, sc, zs, z, wk, d);
         else
-            accum16_one<false, false>(acc, qv, s, zs, z, wk, d);
+            accum16_one<false, false, SIGNED>(acc, qv, sc, zs, z, wk, d);
     };
     for (int base = 0; base < K; base += 64) {
         const int tr = cr.r0;
@@ -169,30 +182,36 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
         const int n = min(64, K - base);
         // one wave-uniform decision per chunk: if every client of the chunk takes
         // the common path (exact fl(z*s) and the fast division), the streaming loop
-        // carries that path alone (fewer registers, no per-client branch)
-        const float ls = tsz.x, lz = tsz.y + zadj, lzs = lz * ls;
+        // carries that path alone, reading (scale, -fl(z*s)) straight from the table
+        const float ls = tsz.x, lz = tsz.y, lzs = lz * ls;
         const bool lfast = __builtin_fmaf(lz, ls, -lzs) == 0.f && d.fast && scale_fast(ls * tw);
         const bool allfast = __ballot(!lfast && __lane_id() < n) == 0;
-        auto fetch = [&](int j, u32x4 &qv, float &sc, float &z, float &wk) {
+        const float tnzs = -lzs;
+        auto fetch = [&](int j, u32x4 &qv, float &sc, float &zz, float &wk, bool common) {
             const int64_t r = readlane_i(tr, j);
-            qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
-            if (SIGNED) qv ^= 0x80808080u;  // int8 q read as the unsigned byte q + 128
+            // wave-uniform row base in a buffer descriptor (SALU), lane offset in a
+            // VGPR: buffer_load ... offen nt, no VALU address arithmetic per client
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(Q + r * ldq), 0, 0x7fffffff, 0x00020000);
+            qv = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff, 0, 2 /* nt */);
             wk = readlane_f(tw, j);
             sc = readlane_f(tsz.x, j);
-            z = readlane_f(tsz.y, j) + zadj;
+            zz = common ? readlane_f(tnzs, j) : readlane_f(tsz.y, j);  // -z*s or z
         };
         auto run = [&](auto common_only) {
-            auto step = [&](const u32x4 qv, float sc, float z, float wk) {
-                if constexpr (decltype(common_only)::value)
-                    accum16_one<true, true>(acc, qv, sc, z * sc, z, wk, d);
+            constexpr bool COMMON = decltype(common_only)::value;
+            auto step = [&](const u32x4 qv, float sc, float zz, float wk) {
+                if constexpr (COMMON)
+                    accum16_one<true, true, SIGNED>(acc, qv, sc, -zz, 0.f, wk, d);
                 else
-                    one(qv, sc, z, wk);
+                    one(qv, sc, zz, wk);
             };
             chunk_pipeline<U, Batch>(
                 n,
                 [&](int j0, Batch &bt) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u) fetch(j0 + u, bt.qv[u], bt.s[u], bt.z[u], bt.wk[u]);
+                    for (int u = 0; u < U; ++u)
+                        fetch(j0 + u, bt.qv[u], bt.s[u], bt.z[u], bt.wk[u], COMMON);
                 },
                 [&](const Batch &bt) {
 #pragma unroll
@@ -200,9 +219,9 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
                 },
                 [&](int j) {
                     u32x4 qv;
-                    float sc, z, wk;
-                    fetch(j, qv, sc, z, wk);
-                    step(qv, sc, z, wk);
+                    float sc, zz, wk;
+                    fetch(j, qv, sc, zz, wk, COMMON);
+                    step(qv, sc, zz, wk);
                 });
         };
         if (allfast)
@@ -405,11 +424,11 @@ __global__ __launch_bounds__(kBlock) void k_dequant_fast(
     float acc[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = -0.f;
-    const uint8_t *Qt = Q + wt.t.src + wt.ec;
+    const uint32_t qoff = (uint32_t)(wt.t.src + wt.ec);  // ldq < 4 GiB (host check)
     if (wt.t.kind == 1)
-        int_one_channel<true>(acc, Qt, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+        int_one_channel<true>(acc, Q, qoff, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
     else
-        int_one_channel<false>(acc, Qt, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+        int_one_channel<false>(acc, Q, qoff, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
     store16(wt, acc, out);
 }
 
@@ -642,6 +661,9 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_
     DLS_REQUIRE(ldq % 16 == 0 && ldf % 4 == 0 && aligned16(out) && (!Q || aligned16(Q)) &&
                     (!F || aligned16(F)),
                 DLS_ELAYOUT, "dls_dequant_fedavg: ldq %% 16, ldf %% 4, 16-byte alignment");
+    DLS_REQUIRE(ldq < ((int64_t)1 << 32), DLS_ELAYOUT,
+                "dls_dequant_fedavg: ldq=%lld must be < 2^32 (32-bit lane offsets)",
+                (long long)ldq);
     const FastDiv d = make_fastdiv(total);
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
