@@ -19,6 +19,9 @@ constexpr int kBlock = 256;
 #ifndef DLS_QUANT_U
 #define DLS_QUANT_U 2  // clients per batch; two batches in flight per lane
 #endif
+#ifndef DLS_QUANT_STORE
+#define DLS_QUANT_STORE 2  // fast-kernel output: 0 plain, 1 non-temporal (-5 %), 2 LDS-coalesced
+#endif
 #ifndef DLS_QUANT_SCHED
 #define DLS_QUANT_SCHED 2  // element pairs between scheduling barriers (0: none)
 #endif
@@ -429,7 +432,37 @@ __global__ __launch_bounds__(kBlock) void k_dequant_fast(
         int_one_channel<true>(acc, Q, qoff, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
     else
         int_one_channel<false>(acc, Q, qoff, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+#if DLS_QUANT_STORE == 2
+    // transpose through LDS so that each store instruction writes 1 KiB contiguous
+    __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
+    float *mine = xs[threadIdx.x >> 6];
+    if (wt.e0 + 16 > wt.t.len) {  // tensor tail: keep the row padding zero
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = (wt.e0 + e < wt.t.len) ? acc[e] : 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+        *reinterpret_cast<f32x4 *>(mine + 16 * __lane_id() + 4 * v) =
+            f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int e = 256 * v + 4 * __lane_id();
+        const f32x4 x = *reinterpret_cast<const f32x4 *>(mine + e);
+        if (e < wt.lenpad) *reinterpret_cast<f32x4 *>(out + wt.t.dst + e) = x;
+    }
+#elif DLS_QUANT_STORE == 1
+    if (!wt.active) return;
+    if (wt.e0 + 16 > wt.t.len) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = (wt.e0 + e < wt.t.len) ? acc[e] : 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+        __builtin_nontemporal_store(f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]},
+                                    reinterpret_cast<f32x4 *>(out + wt.t.dst + wt.e0) + v);
+#else
     store16(wt, acc, out);
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
