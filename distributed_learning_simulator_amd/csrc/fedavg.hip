@@ -4,7 +4,9 @@
 // (one 16-byte load per client), walks the K clients in the reference's
 // iteration order and keeps the running sum in registers, so every client byte
 // is read once and the 4*P-byte result is written once.  HBM-bound: the
-// algorithmic traffic of one call is K*P*4 + P*4 bytes.
+// algorithmic traffic of one call is K*P*4 + P*4 bytes.  The client rows and
+// weights reach the wave through per-lane tables and v_readlane, and batches
+// of DLS_FEDAVG_PIPE_U clients are double-buffered (k_fedavg_exact_pipe).
 //
 // EXACT mode reproduces the reference op sequence bit-for-bit:
 //     term_i = fl(fl(x * fl32(n_i)) / fl32(N)); acc = term_0; acc = fl(acc + term_i)
@@ -16,12 +18,6 @@ namespace dls {
 namespace {
 
 constexpr int kBlock = 256;
-#ifndef DLS_FEDAVG_UNROLL
-#define DLS_FEDAVG_UNROLL 8
-#endif
-#ifndef DLS_FEDAVG_PIPE
-#define DLS_FEDAVG_PIPE 1
-#endif
 #ifndef DLS_FEDAVG_PIPE_U
 #define DLS_FEDAVG_PIPE_U 4
 #endif
@@ -57,28 +53,6 @@ __device__ __forceinline__ f32x4 term4(f32x4 x, float w, const FastDiv &d) {
 
 __device__ __forceinline__ f32x4 add4(f32x4 a, f32x4 b) {
     return a + b;
-}
-
-template <int UNROLL, bool NT>
-__global__ __launch_bounds__(kBlock) void k_fedavg_exact(const f32x4 *__restrict__ U,
-                                                         int64_t ldu4,
-                                                         const int32_t *__restrict__ rows,
-                                                         const float *__restrict__ w, int K,
-                                                         FastDiv d, int64_t P4,
-                                                         f32x4 *__restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= P4) return;
-    f32x4 acc = term4(load4<NT>(U + (int64_t)rows[0] * ldu4 + i), w[0], d);
-    int j = 1;
-    for (; j + UNROLL <= K; j += UNROLL) {
-        f32x4 x[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) x[u] = load4<NT>(U + (int64_t)rows[j + u] * ldu4 + i);
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) acc = add4(acc, term4(x[u], w[j + u], d));
-    }
-    for (; j < K; ++j) acc = add4(acc, term4(load4<NT>(U + (int64_t)rows[j] * ldu4 + i), w[j], d));
-    out[i] = acc;
 }
 
 // Software-pipelined form.  Clients are taken in chunks of 64: lane j holds
@@ -241,14 +215,9 @@ extern "C" int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows,
     hipStream_t st = as_stream(stream);
     if (mode == DLS_FEDAVG_EXACT) {
         const FastDiv d = make_fastdiv(total);
-        if (DLS_FEDAVG_PIPE)
-            hipLaunchKernelGGL((k_fedavg_exact_pipe<DLS_FEDAVG_PIPE_U, true>), grid, dim3(kBlock), 0,
-                               st, reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight,
-                               (int)K, d, P4, reinterpret_cast<f32x4 *>(out));
-        else
-            hipLaunchKernelGGL((k_fedavg_exact<DLS_FEDAVG_UNROLL, true>), grid, dim3(kBlock), 0, st,
-                               reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K,
-                               d, P4, reinterpret_cast<f32x4 *>(out));
+        hipLaunchKernelGGL((k_fedavg_exact_pipe<DLS_FEDAVG_PIPE_U, true>), grid, dim3(kBlock), 0, st,
+                           reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, d,
+                           P4, reinterpret_cast<f32x4 *>(out));
     } else if (mode == DLS_FEDAVG_FMA) {
         hipLaunchKernelGGL((k_fedavg_fma<8, true>), grid, dim3(kBlock), 0, st,
                            reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, total,
