@@ -195,7 +195,7 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
             // wave-uniform row base in a buffer descriptor (SALU), lane offset in a
             // VGPR: buffer_load ... offen nt, no VALU address arithmetic per client
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint8_t *>(Q + r * ldq), 0, 0x7fffffff, 0x00020000);
+                const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB range
             qv = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff, 0, 2 /* nt */);
             wk = readlane_f(tw, j);
             sc = readlane_f(tsz.x, j);
