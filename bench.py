@@ -243,8 +243,8 @@ def bench_quant(args, dev):
     g = torch.Generator(device=dev).manual_seed(SEED + 4)
     store.Q.random_(0, 256, generator=g)  # int8 payload bytes
     store.F.normal_(generator=g).mul_(0.01)
-    store.sz[:, :, 0].uniform_(1e-4, 1e-2, generator=g)
-    store.sz[:, :, 1].zero_()
+    store.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
+    store.sz[..., 1].zero_()
     rows = list(range(K))
     store._free = []
     n = torch.randint(100, 1001, (K,), generator=g, device=dev).tolist()

@@ -44,6 +44,14 @@ __device__ __forceinline__ float readlane_f(float v, int j) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
 }
 
+// (scale, zero point) pairs: pair of (client row r, channel c) at
+// sz[r * row + c * chan] (strides in pairs).  The store keeps them channel-major
+// (chan = capacity, row = 1), so a wave's per-chunk table load for its channel
+// reads 64 consecutive pairs instead of 64 lines 107 KB apart.
+struct SzLayout {
+    int64_t row, chan;
+};
+
 // --------------------------------------------------------- client pipeline
 // Clients are walked in chunks of 64.  Lane j holds client (base + j)'s row
 // and weight (one coalesced vector load per field and chunk, fetched a chunk
@@ -150,7 +158,7 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
 template <bool SIGNED>
 __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t *__restrict__ Q,
                                                 uint32_t qoff, int64_t ldq,
-                                                const f32x2 *__restrict__ szc, int64_t ldc,
+                                                const f32x2 *__restrict__ szc, SzLayout L,
                                                 const int32_t *__restrict__ rows,
                                                 const float *__restrict__ w, int K,
                                                 const FastDiv &d) {
@@ -164,7 +172,7 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
     };
     ChunkRows cr;
     cr.init(rows, w, K);
-    f32x2 nsz = szc[(int64_t)cr.r0 * ldc];  // this wave's channel, client 64c + lane
+    f32x2 nsz = szc[(int64_t)cr.r0 * L.row];  // this wave's channel, client 64c + lane
     auto one = [&](const u32x4 qv, float sc, float z, float wk) {
         const float zs = z * sc;
         const bool zfma = __builtin_fmaf(z, sc, -zs) == 0.f;  // fl(z*s) exact
@@ -180,7 +188,7 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
         const int tr = cr.r0;
         const float tw = cr.w0;
         const f32x2 tsz = nsz;
-        nsz = szc[(int64_t)cr.r1 * ldc];  // next chunk (its rows landed a chunk ago)
+        nsz = szc[(int64_t)cr.r1 * L.row];  // next chunk (its rows landed a chunk ago)
         cr.advance(rows, w, K, base);
         const int n = min(64, K - base);
         // one wave-uniform decision per chunk: if every client of the chunk takes
@@ -239,7 +247,7 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
 template <bool SIGNED>
 __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_t *__restrict__ Qt,
                                                   int64_t ldq, const f32x2 *__restrict__ szc,
-                                                  int64_t ldc, int split,
+                                                  SzLayout L, int split,
                                                   const int32_t *__restrict__ rows,
                                                   const float *__restrict__ w, int K,
                                                   const FastDiv &d) {
@@ -257,8 +265,8 @@ __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_
             const float wk = readlane_f(tw, j);
             u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
             if (SIGNED) qv ^= 0x80808080u;
-            const f32x2 a = szc[r * ldc];
-            const f32x2 b = two ? szc[r * ldc + 1] : a;
+            const f32x2 a = szc[r * L.row];
+            const f32x2 b = two ? szc[r * L.row + L.chan] : a;
             const float za = a.y + zadj, zb = b.y + zadj;
             const bool fast = d.fast && scale_fast(a.x * wk) && scale_fast(b.x * wk);
 #pragma unroll
@@ -280,7 +288,7 @@ __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_
 template <bool SIGNED>
 __device__ __forceinline__ void int_lane_pipelined(float (&acc)[16], const uint8_t *__restrict__ Qt,
                                                    int64_t ldq, const f32x2 *__restrict__ szl,
-                                                   int64_t ldc, const int32_t *__restrict__ rows,
+                                                   SzLayout L, const int32_t *__restrict__ rows,
                                                    const float *__restrict__ w, int K,
                                                    const FastDiv &d) {
     constexpr int U = DLS_QUANT_U;
@@ -314,7 +322,7 @@ __device__ __forceinline__ void int_lane_pipelined(float (&acc)[16], const uint8
             const int64_t r = readlane_i(tr, j);
             qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
             if (SIGNED) qv ^= 0x80808080u;  // int8 q read as the unsigned byte q + 128
-            sz = szl[r * ldc];
+            sz = szl[r * L.row];
             wk = readlane_f(tw, j);
         };
         chunk_pipeline<U, Batch>(
@@ -341,7 +349,7 @@ __device__ __forceinline__ void int_lane_pipelined(float (&acc)[16], const uint8
 template <bool SIGNED>
 __device__ __forceinline__ void int_tiny_rows(float (&acc)[16], const uint8_t *__restrict__ Qt,
                                               int64_t ldq, const f32x2 *__restrict__ sz,
-                                              int64_t ldc, const int (&cj)[16],
+                                              SzLayout L, const int (&cj)[16],
                                               const int32_t *__restrict__ rows,
                                               const float *__restrict__ w, int K,
                                               const FastDiv &d) {
@@ -353,7 +361,7 @@ __device__ __forceinline__ void int_tiny_rows(float (&acc)[16], const uint8_t *_
         const float wk = w[k];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const f32x2 a = sz[row * ldc + cj[e]];
+            const f32x2 a = sz[row * L.row + cj[e] * L.chan];
             const float t = ((byte_f32(qv[e >> 2], e & 3) - (a.y + zadj)) * a.x) * wk;
             acc[e] += (d.fast && scale_fast(a.x * wk)) ? markstein(t, d.b, d.y) : t / d.b;
         }
@@ -420,7 +428,7 @@ __device__ __forceinline__ void store16(const WaveTile &wt, float (&acc)[16],
 
 __global__ __launch_bounds__(kBlock) void k_dequant_fast(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
-    const f32x2 *__restrict__ sz, int64_t ldc, const int32_t *__restrict__ rows,
+    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
     const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
@@ -429,9 +437,9 @@ __global__ __launch_bounds__(kBlock) void k_dequant_fast(
     for (int e = 0; e < 16; ++e) acc[e] = -0.f;
     const uint32_t qoff = (uint32_t)(wt.t.src + wt.ec);  // ldq < 4 GiB (host check)
     if (wt.t.kind == 1)
-        int_one_channel<true>(acc, Q, qoff, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+        int_one_channel<true>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
     else
-        int_one_channel<false>(acc, Q, qoff, ldq, sz + wt.t.chan0, ldc, rows, w, K, d);
+        int_one_channel<false>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
 #if DLS_QUANT_STORE == 2
     // transpose through LDS so that each store instruction writes 1 KiB contiguous
     __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
@@ -467,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_fast(
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
-    const float *__restrict__ F, int64_t ldf, const f32x2 *__restrict__ sz, int64_t ldc,
+    const float *__restrict__ F, int64_t ldf, const f32x2 *__restrict__ sz, SzLayout L,
     const int32_t *__restrict__ rows, const float *__restrict__ w, int K, FastDiv d,
     float *__restrict__ out) {
     WaveTile wt;
@@ -487,13 +495,13 @@ __global__ __launch_bounds__(kBlock) void k_dequant_general(
             const int split = t.row_len - p % t.row_len;  // [0, split) in c, rest in c + 1
             if (__ballot(split < 16) == 0) {  // wave-uniform: no lane straddles a channel
                 if (sgn)
-                    int_lane_pipelined<true>(acc, Qt, ldq, sz + c, ldc, rows, w, K, d);
+                    int_lane_pipelined<true>(acc, Qt, ldq, sz + c * L.chan, L, rows, w, K, d);
                 else
-                    int_lane_pipelined<false>(acc, Qt, ldq, sz + c, ldc, rows, w, K, d);
+                    int_lane_pipelined<false>(acc, Qt, ldq, sz + c * L.chan, L, rows, w, K, d);
             } else if (sgn) {
-                int_lane_channels<true>(acc, Qt, ldq, sz + c, ldc, split, rows, w, K, d);
+                int_lane_channels<true>(acc, Qt, ldq, sz + c * L.chan, L, split, rows, w, K, d);
             } else {
-                int_lane_channels<false>(acc, Qt, ldq, sz + c, ldc, split, rows, w, K, d);
+                int_lane_channels<false>(acc, Qt, ldq, sz + c * L.chan, L, split, rows, w, K, d);
             }
         } else {
             const int r = p % t.row_len;
@@ -501,9 +509,9 @@ __global__ __launch_bounds__(kBlock) void k_dequant_general(
 #pragma unroll
             for (int e = 0; e < 16; ++e) cj[e] = min(c + (r + e) / t.row_len, t.chan_end - 1);
             if (sgn)
-                int_tiny_rows<true>(acc, Qt, ldq, sz, ldc, cj, rows, w, K, d);
+                int_tiny_rows<true>(acc, Qt, ldq, sz, L, cj, rows, w, K, d);
             else
-                int_tiny_rows<false>(acc, Qt, ldq, sz, ldc, cj, rows, w, K, d);
+                int_tiny_rows<false>(acc, Qt, ldq, sz, L, cj, rows, w, K, d);
         }
     }
     store16(wt, acc, out);
@@ -684,7 +692,8 @@ using namespace dls;
 
 extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_t nfast,
                                   const void *Q, int64_t ldq, const float *F, int64_t ldf,
-                                  const float *sz, int64_t ldc, const int32_t *rows,
+                                  const float *sz, int64_t sz_row, int64_t sz_chan,
+                                  const int32_t *rows,
                                   const float *weight, int32_t K, float total, float *out,
                                   dls_stream_t stream) {
     DLS_REQUIRE(tiles && rows && weight && out && sz, DLS_EINVAL,
@@ -698,18 +707,19 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_
                 "dls_dequant_fedavg: ldq=%lld must be < 2^32 (32-bit lane offsets)",
                 (long long)ldq);
     const FastDiv d = make_fastdiv(total);
+    const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
     if (nfast > 0)
         hipLaunchKernelGGL(k_dequant_fast, dim3((unsigned)((nfast + wpb - 1) / wpb)), dim3(kBlock),
                            0, st, tiles, (int)nfast, reinterpret_cast<const uint8_t *>(Q), ldq,
-                           reinterpret_cast<const f32x2 *>(sz), ldc, rows, weight, (int)K, d, out);
+                           reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
     const int ngen = ntiles - nfast;
     if (ngen > 0)
         hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
                            dim3(kBlock), 0, st, tiles + nfast, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
-                           reinterpret_cast<const f32x2 *>(sz), ldc, rows, weight, (int)K, d, out);
+                           reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
     return check_launch("dls_dequant_fedavg");
 }
 

@@ -11,7 +11,9 @@ HBM layout per client row:
                              the row pitch ldq on 256-B boundaries, so a wavefront's
                              1 KiB load per client covers exactly 8 cache lines
   F  fp32  [capacity, ldf]   fp32 tensors (biases ...), 64-element aligned
-  sz fp32  [capacity, C+1, 2] per output channel (fl32(scale), zero_point)
+  sz fp32  [C+1, capacity, 2] (fl32(scale), zero_point) per output channel,
+                             channel-major: a wave's per-channel table load for 64
+                             clients reads 512 consecutive bytes
 and a tile table (``dls_qtile``) built once per layout: wave tiles of <= 1024
 elements inside one tensor, which also carry the channel bookkeeping; the
 tiles whose elements all lie in one output channel come first (``nfast``) and
@@ -122,7 +124,7 @@ class QuantizedClientStore:
         ql = self.qlayout
         self.Q = torch.zeros((cap, ql.ldq), dtype=torch.uint8, device=self.device)
         self.F = torch.zeros((cap, ql.ldf), dtype=torch.float32, device=self.device)
-        self.sz = torch.zeros((cap, ql.C + 1, 2), dtype=torch.float32, device=self.device)
+        self.sz = torch.zeros((ql.C + 1, cap, 2), dtype=torch.float32, device=self.device)
         t, self.nfast = ql.tiles()
         self.ntiles = len(t)
         self.tiles = torch.from_numpy(t.view(np.uint8).copy()).to(self.device)
@@ -140,12 +142,12 @@ class QuantizedClientStore:
                                  device=self.device)
             self.F = torch.zeros((cap,) + tuple(old[1].shape[1:]), dtype=old[1].dtype,
                                  device=self.device)
-            self.sz = torch.zeros((cap,) + tuple(old[2].shape[1:]), dtype=old[2].dtype,
+            self.sz = torch.zeros((old[2].shape[0], cap, 2), dtype=old[2].dtype,
                                   device=self.device)
             n = old[0].shape[0]
             self.Q[:n].copy_(old[0])
             self.F[:n].copy_(old[1])
-            self.sz[:n].copy_(old[2])
+            self.sz[:, :n].copy_(old[2])
             self._free = list(range(n, cap))[::-1]
         return self._free.pop()
 
@@ -166,8 +168,8 @@ class QuantizedClientStore:
                 # before the fp32 ops (servers/fed_quant_server.py:31)
                 s32 = torch.as_tensor(scale).reshape(-1).to(torch.float32)
                 z32 = torch.as_tensor(zp).reshape(-1).to(torch.float32)
-                self.sz[row, cb:cb + C, 0].copy_(s32, non_blocking=True)
-                self.sz[row, cb:cb + C, 1].copy_(z32, non_blocking=True)
+                self.sz[cb:cb + C, row, 0].copy_(s32, non_blocking=True)
+                self.sz[cb:cb + C, row, 1].copy_(z32, non_blocking=True)
             else:
                 self.F[row, ql.src[i]:ql.src[i] + n].copy_(v.reshape(-1).float(),
                                                            non_blocking=True)

@@ -154,12 +154,13 @@ typedef struct dls_qtile {
  *   out[e] (+)= fl(fl(fl(fl(q - zp[c]) * scale[c]) * n_i) / N)  (int tensors)
  *   out[e] (+)= fl(fl(x * n_i) / N)                              (fp32 tensors)
  * bit-exact in client order.  Q int8/uint8 [*, ldq], F fp32 [*, ldf],
- * sz fp32 pairs [*, ldc] of (fl32(scale), zero_point) per channel.  Tiles
+ * sz fp32 pairs (fl32(scale), zero_point): client row r, channel c at pair
+ * r * sz_row + c * sz_chan (the store keeps them channel-major: sz_row = 1).  Tiles
  * [0, nfast) must be one-channel int tiles (see dls_qtile). */
 int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_t nfast, const void *Q,
-                       int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t ldc,
-                       const int32_t *rows, const float *weight, int32_t K, float total,
-                       float *out, dls_stream_t stream);
+                       int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t sz_row,
+                       int64_t sz_chan, const int32_t *rows, const float *weight, int32_t K,
+                       float total, float *out, dls_stream_t stream);
 
 /* Per-segment min / max of x over [seg_off[s], seg_off[s+1]) (torch.aminmax);
  * seg_off is device int64 [nseg+1] with seg_off[nseg] == total.  NaNs are

@@ -81,21 +81,23 @@ def setup(dev):
     st = QuantizedClientStore(template, dev, capacity=100)
     st.Q.random_(0, 256, generator=g)
     st.F.normal_(generator=g)
-    st.sz[:, :, 0].uniform_(1e-4, 1e-2, generator=g)
-    st.sz[:, :, 1].zero_()
+    st.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
+    st.sz[..., 1].zero_()
     qo = torch.empty(st.layout.P, device=dev)
     ql = st.qlayout
     Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
     Pf = sum(m for m, k in zip(st.layout.numels, ql.kinds) if not k)
     W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, st.nfast, ptr(st.Q), st.Q.stride(0),
                                                  ptr(st.F), st.F.stride(0), ptr(st.sz),
-                                                 st.sz.stride(0) // 2, ptr(rows), ptr(w), 100, tot,
+                                                 st.sz.stride(1) // 2, st.sz.stride(0) // 2,
+                                                 ptr(rows), ptr(w), 100, tot,
                                                  ptr(qo), stream()),
                   100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
     rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
     W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, st.nfast,
                                                          ptr(st.Q), st.Q.stride(0),
                                                          ptr(st.F), st.F.stride(0), ptr(st.sz),
+                                                         st.sz.stride(1) // 2,
                                                          st.sz.stride(0) // 2, ptr(rows0), ptr(w),
                                                          100, tot, ptr(qo), stream()),
                           100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
