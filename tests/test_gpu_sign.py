@@ -200,3 +200,33 @@ def test_fused_vote_planes_match_two_stage(P, K):
     v3 = torch.zeros(Wd, dtype=torch.int64, device=dev)  # packed vote alone
     _native.sign_vote(planes, None, K, Pp, None, vote_planes=v3)
     assert torch.equal(v3, v2)
+
+
+def test_vote_wide_tiles_rows_and_padding():
+    """Large models take the 4-groups-per-lane vote; its last block holds live groups,
+    padding groups (ngroups <= g < vote_groups) and groups past the end."""
+    from distributed_learning_simulator_amd import _native
+    K, P = 20, 9_000_004  # ngroups 140626, vote_groups 140628: 550 blocks of 256 groups
+    Wd = _native.sign_words(P)
+    g = torch.Generator(device=dev).manual_seed(11)
+    planes = torch.randint(-2**62, 2**62, (K, Wd), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]
+    planes[3, 2 * 140620 + 1] |= planes[3, 2 * 140620]  # NaN codes in the tail group
+    planes[:, 2 * (P // 64) + 1:] = 0  # bits past P are zero, as the packer leaves them
+    planes[:, 2 * (P // 64)] &= (1 << (P % 64)) - 1
+    planes[:, 2 * (P // 64) + 1] = 0
+    rows = torch.tensor([19, 4, 3, 11, 0, 7, 8, 15, 2, 16, 9, 12, 5], dtype=torch.int32, device=dev)
+    counts = torch.empty(P, dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, rows, len(rows), P, counts)
+    w = planes.cpu().numpy().view(np.uint64)
+    S = np.stack([osign.unpack_planes(w[r], P) for r in rows.tolist()])
+    assert np.array_equal(counts.cpu().numpy(), osign.vote_counts(S))
+    sign = torch.empty(P, device=dev)
+    vp = torch.full((Wd,), 0x55, dtype=torch.int64, device=dev)
+    _native.sign_vote(planes, rows, len(rows), P, sign, vote_planes=vp)
+    s2 = torch.empty(P, device=dev)
+    v2 = torch.zeros(Wd, dtype=torch.int64, device=dev)
+    _native.sign_from_counts(counts, P, s2, v2)
+    assert same_bits(sign.cpu().numpy(), s2.cpu().numpy())
+    assert torch.equal(vp, v2)
+    assert same_bits(sign.cpu().numpy(), osign.majority_vote(S))
