@@ -44,7 +44,7 @@ def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def setup(dev):
+def setup(dev, want=()):
     W = {}
     lay = ParameterLayout(resnet18_cifar())
     P = lay.P
@@ -56,6 +56,13 @@ def setup(dev):
     tot = float(w.sum())
     W["fedavg"] = (lambda L: L.dls_fedavg_f32(ptr(U), P, ptr(rows), ptr(w), 100, tot, P, 0,
                                               ptr(out), stream()), 100 * P * 4 + P * 4)
+    if "fedavg1k" in want:  # 1000 clients (45 GB of rows)
+        U1 = torch.empty((1000, P), device=dev).normal_(generator=g).mul_(0.05)
+        r1 = torch.arange(1000, dtype=torch.int32, device=dev)
+        w1 = torch.randint(100, 1000, (1000,), generator=g, device=dev).float()
+        t1 = float(w1.sum())
+        W["fedavg1k"] = (lambda L: L.dls_fedavg_f32(ptr(U1), P, ptr(r1), ptr(w1), 1000, t1, P, 0,
+                                                    ptr(out), stream()), 1000 * P * 4 + P * 4)
     Wd = _native.sign_words(P)
     planes = torch.randint(-2**62, 2**62, (1000, Wd), generator=g, device=dev)
     planes[:, 1::2] &= ~planes[:, 0::2]
@@ -121,7 +128,7 @@ def main():
             for p in sorted(glob.glob(os.path.join(
                 os.environ.get("DLS_VARIANTS", os.path.join(ROOT, "tools", "_variants")),
                 "libdls_*.so")))}
-    W = setup(dev)
+    W = setup(dev, args.workloads.split(","))
     res = {}
     for wl in args.workloads.split(","):
         fn, nbytes = W[wl]
