@@ -57,7 +57,7 @@ SIGNATURES = {
     "dls_sign_vote": ([_p, _i64, _p, _i32, _i64, _p, _p, _p, _p], _i32),
     "dls_sign_sgd_direction": ([_p, _p, _i64, _f32, _f32, _i32, _i32, _p, _p, _p], _i32),
     "dls_sign_sgd_apply": ([_p, _p, _i64, _f32, _f32, _p], _i32),
-    "dls_dequant_fedavg": ([_p, _i32, _i32, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _p, _i32, _f32,
+    "dls_dequant_fedavg": ([_p, _i32, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _p, _i32, _f32,
                             _p, _p],
                            _i32),
     "dls_segment_minmax_f32": ([_p, _p, _i32, _p, _p, _i64, _p], _i32),
@@ -189,11 +189,14 @@ def sign_sgd_apply(param, vote_planes, neg_lr, weight_decay, stream=None):
 # ----------------------------------------------------------------------- quant
 def dequant_fedavg(tiles, ntiles, nfast, Q, F, sz, rows, weight, total, out, sz_strides=None,
                    stream=None):
-    """sz: (scale, zero point) pairs; sz_strides = (row, channel) strides in pairs
-    (default: a channel-major [C+1, capacity, 2] tensor)."""
+    """nfast: 4 counts of one-channel tiles with 4, 3, 2, 1 KiB slices at the head of
+    the table (quant_store.QuantLayout.tiles()); sz: (scale, zero point) pairs;
+    sz_strides = (row, channel) strides in pairs (default: a channel-major
+    [C+1, capacity, 2] tensor)."""
+    nf = (ctypes.c_int32 * 4)(*[int(x) for x in nfast])
     if sz_strides is None:
         sz_strides = (sz.stride(1) // 2, sz.stride(0) // 2)
-    _check(lib().dls_dequant_fedavg(_ptr(tiles), ntiles, nfast, _ptr(Q),
+    _check(lib().dls_dequant_fedavg(_ptr(tiles), ntiles, nf, _ptr(Q),
                                     Q.stride(0) if Q is not None else 0,
                                     _ptr(F), F.stride(0) if F is not None else 0, _ptr(sz),
                                     int(sz_strides[0]), int(sz_strides[1]), _ptr(rows),

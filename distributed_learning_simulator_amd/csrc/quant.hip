@@ -19,8 +19,8 @@ constexpr int kBlock = 256;
 #ifndef DLS_QUANT_U
 #define DLS_QUANT_U 2  // clients per batch; two batches in flight per lane
 #endif
-#ifndef DLS_QUANT_STORE
-#define DLS_QUANT_STORE 2  // fast-kernel output: 0 plain, 1 non-temporal (-5 %), 2 LDS-coalesced
+#ifndef DLS_QUANT_UG
+#define DLS_QUANT_UG 1  // clients per batch on multi-KiB tiles
 #endif
 #ifndef DLS_QUANT_SCHED
 #define DLS_QUANT_SCHED 2  // element pairs between scheduling barriers (0: none)
@@ -155,35 +155,25 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
     }
 }
 
-template <bool SIGNED>
-__device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t *__restrict__ Q,
-                                                uint32_t qoff, int64_t ldq,
+template <int U, int GN>
+struct QBatch {
+    u32x4 qv[U][GN];
+    float s[U], z[U], wk[U];
+};
+
+template <bool SIGNED, int G>
+__device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8_t *__restrict__ Q,
+                                                const uint32_t (&qoff)[G], int64_t ldq,
                                                 const f32x2 *__restrict__ szc, SzLayout L,
                                                 const int32_t *__restrict__ rows,
                                                 const float *__restrict__ w, int K,
                                                 const FastDiv &d) {
     // int8 bytes convert sign-extended (value q, zero point zp); uint8 bytes
     // unsigned.  The payload address is (Q + row*ldq) [wave-uniform, SALU] +
-    // qoff [this lane's 32-bit offset].
-    constexpr int U = DLS_QUANT_U;
-    struct Batch {
-        u32x4 qv[U];
-        float s[U], z[U], wk[U];
-    };
+    // qoff[g] [this lane's 32-bit offset in KiB slice g of the tile].
     ChunkRows cr;
     cr.init(rows, w, K);
     f32x2 nsz = szc[(int64_t)cr.r0 * L.row];  // this wave's channel, client 64c + lane
-    auto one = [&](const u32x4 qv, float sc, float z, float wk) {
-        const float zs = z * sc;
-        const bool zfma = __builtin_fmaf(z, sc, -zs) == 0.f;  // fl(z*s) exact
-        const bool fast = d.fast && scale_fast(sc * wk);
-        if (__builtin_expect(zfma && fast, 1))
-            accum16_one<true, true, SIGNED>(acc, qv, sc, zs, z, wk, d);
-        else if (fast)
-            accum16_one<false, true, SIGNED>(acc, qv, sc, zs, z, wk, d);
-        else
-            accum16_one<false, false, SIGNED>(acc, qv, sc, zs, z, wk, d);
-    };
     for (int base = 0; base < K; base += 64) {
         const int tr = cr.r0;
         const float tw = cr.w0;
@@ -198,47 +188,79 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[16], const uint8_t 
         const bool lfast = __builtin_fmaf(lz, ls, -lzs) == 0.f && d.fast && scale_fast(ls * tw);
         const bool allfast = __ballot(!lfast && __lane_id() < n) == 0;
         const float tnzs = -lzs;
-        auto fetch = [&](int j, u32x4 &qv, float &sc, float &zz, float &wk, bool common) {
-            const int64_t r = readlane_i(tr, j);
-            // wave-uniform row base in a buffer descriptor (SALU), lane offset in a
-            // VGPR: buffer_load ... offen nt, no VALU address arithmetic per client
-            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB range
-            qv = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff, 0, 2 /* nt */);
-            wk = readlane_f(tw, j);
-            sc = readlane_f(tsz.x, j);
-            zz = common ? readlane_f(tnzs, j) : readlane_f(tsz.y, j);  // -z*s or z
-        };
-        auto run = [&](auto common_only) {
+        // slices [G0, G0 + GN) of the tile, clients of this chunk
+        auto run = [&](auto common_only, auto g0, auto gn) {
             constexpr bool COMMON = decltype(common_only)::value;
-            auto step = [&](const u32x4 qv, float sc, float zz, float wk) {
-                if constexpr (COMMON)
-                    accum16_one<true, true, SIGNED>(acc, qv, sc, -zz, 0.f, wk, d);
-                else
-                    one(qv, sc, zz, wk);
-            };
-            chunk_pipeline<U, Batch>(
-                n,
-                [&](int j0, Batch &bt) {
+            constexpr int G0 = decltype(g0)::value, GN = decltype(gn)::value;
+            constexpr int U = GN > 1 ? DLS_QUANT_UG : DLS_QUANT_U;  // clients per batch
+            auto fetch = [&](int j, u32x4 (&qv)[GN], float &sc, float &zz, float &wk) {
+                const int64_t r = readlane_i(tr, j);
+                // wave-uniform row base in a buffer descriptor (SALU), lane offset in
+                // a VGPR: buffer_load ... offen nt, no VALU address arithmetic per client
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
 #pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        fetch(j0 + u, bt.qv[u], bt.s[u], bt.z[u], bt.wk[u], COMMON);
+                for (int g = 0; g < GN; ++g)
+                    qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[G0 + g], 0, 2 /* nt */);
+                wk = readlane_f(tw, j);
+                sc = readlane_f(tsz.x, j);
+                zz = COMMON ? readlane_f(tnzs, j) : readlane_f(tsz.y, j);  // -z*s or z
+            };
+            auto step = [&](const u32x4 (&qv)[GN], float sc, float zz, float wk) {
+                if constexpr (COMMON) {
+#pragma unroll
+                    for (int g = 0; g < GN; ++g)
+                        accum16_one<true, true, SIGNED>(acc[G0 + g], qv[g], sc, -zz, 0.f, wk, d);
+                } else {
+                    const float zs = zz * sc;
+                    const bool zfma = __builtin_fmaf(zz, sc, -zs) == 0.f;  // fl(z*s) exact
+                    const bool fast = d.fast && scale_fast(sc * wk);
+                    // client-uniform path choice, outside the slice loop
+                    if (__builtin_expect(zfma && fast, 1)) {
+#pragma unroll
+                        for (int g = 0; g < GN; ++g)
+                            accum16_one<true, true, SIGNED>(acc[G0 + g], qv[g], sc, zs, zz, wk, d);
+                    } else if (fast) {
+#pragma unroll
+                        for (int g = 0; g < GN; ++g)
+                            accum16_one<false, true, SIGNED>(acc[G0 + g], qv[g], sc, zs, zz, wk, d);
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < GN; ++g)
+                            accum16_one<false, false, SIGNED>(acc[G0 + g], qv[g], sc, zs, zz, wk, d);
+                    }
+                }
+            };
+            chunk_pipeline<U, QBatch<U, GN>>(
+                n,
+                [&](int j0, QBatch<U, GN> &bt) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) fetch(j0 + u, bt.qv[u], bt.s[u], bt.z[u], bt.wk[u]);
                 },
-                [&](const Batch &bt) {
+                [&](const QBatch<U, GN> &bt) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) step(bt.qv[u], bt.s[u], bt.z[u], bt.wk[u]);
                 },
                 [&](int j) {
-                    u32x4 qv;
+                    u32x4 qv[GN];
                     float sc, zz, wk;
-                    fetch(j, qv, sc, zz, wk, COMMON);
+                    fetch(j, qv, sc, zz, wk);
                     step(qv, sc, zz, wk);
                 });
         };
-        if (allfast)
-            run(std::true_type{});
-        else
-            run(std::false_type{});
+        using I0 = std::integral_constant<int, 0>;
+        using IG = std::integral_constant<int, G>;
+        using I1 = std::integral_constant<int, 1>;
+        if (allfast) {
+            run(std::true_type{}, I0{}, IG{});
+        } else {
+            // rare chunks (inexact fl(z*s), out-of-range scales): one slice at a
+            // time, so that this path's registers stay within the common path's
+            run(std::false_type{}, I0{}, I1{});
+            if constexpr (G > 1) run(std::false_type{}, std::integral_constant<int, 1>{}, I1{});
+            if constexpr (G > 2) run(std::false_type{}, std::integral_constant<int, 2>{}, I1{});
+            if constexpr (G > 3) run(std::false_type{}, std::integral_constant<int, 3>{}, I1{});
+        }
     }
 }
 
@@ -388,11 +410,12 @@ __device__ __forceinline__ void f32_chunk(float (&acc)[16], const float *__restr
     }
 }
 
-// Tiles are wave tiles: <= 1024 elements of one tensor, a lane owns 16
-// consecutive elements; wave w of block b takes tile 4b + w.  The host sorts
-// the table so that the first `nfast` tiles are int tiles inside ONE channel
-// (the bulk of every large-row weight): k_dequant_fast runs only that path,
-// so its register budget is not set by the rare paths of k_dequant_general.
+// Tiles are wave tiles inside one tensor; wave w of block b takes tile 4b + w.
+// The host sorts the table so that the first tiles are int tiles inside ONE
+// channel (the bulk of every large-row weight), grouped by their number of
+// 1 KiB slices (4, 3, 2, 1): one k_dequant_fast<G> launch per group runs only
+// that path, so its register budget is set neither by a wider G nor by the
+// rare paths of k_dequant_general (<= 1024 elements, a lane owns 16).
 // -0 + t == t for every fp32 t, so every accumulator starts at -0 and the
 // first client "is assigned" (servers/fed_server.py:62-65).
 struct WaveTile {
@@ -426,51 +449,65 @@ __device__ __forceinline__ void store16(const WaveTile &wt, float (&acc)[16],
         o[v] = f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
 }
 
-__global__ __launch_bounds__(kBlock) void k_dequant_fast(
-    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
-    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
-    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
-    WaveTile wt;
-    if (!wave_tile(tiles, ntiles, wt)) return;
-    float acc[16];
+// One-channel tiles of up to 4 KiB: slice g of the tile is lanes'
+// 16-element chunks 1024 g + 16 lane; the wave walks the clients once for all
+// its slices (per-client table reads and readlanes amortised over G KiB).
+template <bool SIGNED, int G>
+__device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
+                                          int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
+                                          const int32_t *__restrict__ rows,
+                                          const float *__restrict__ w, int K, const FastDiv &d,
+                                          float *__restrict__ out) {
+    float acc[G][16];
+    uint32_t qoff[G];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = -0.f;
-    const uint32_t qoff = (uint32_t)(wt.t.src + wt.ec);  // ldq < 4 GiB (host check)
-    if (wt.t.kind == 1)
-        int_one_channel<true>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
-    else
-        int_one_channel<false>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
-#if DLS_QUANT_STORE == 2
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[g][e] = -0.f;
+        const int e0 = 1024 * g + 16 * __lane_id();
+        // idle lanes load a valid duplicate (loads stay unconditional)
+        qoff[g] = (uint32_t)(wt.t.src + (e0 < wt.lenpad ? e0 : wt.lenpad - 16));  // ldq < 4 GiB
+    }
+    int_one_channel<SIGNED, G>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
     // transpose through LDS so that each store instruction writes 1 KiB contiguous
     __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
     float *mine = xs[threadIdx.x >> 6];
-    if (wt.e0 + 16 > wt.t.len) {  // tensor tail: keep the row padding zero
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = (wt.e0 + e < wt.t.len) ? acc[e] : 0.f;
+    for (int g = 0; g < G; ++g) {
+        const int e0 = 1024 * g + 16 * __lane_id();
+        if (e0 + 16 > wt.t.len) {  // tensor tail: keep the row padding zero
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[g][e] = (e0 + e < wt.t.len) ? acc[g][e] : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+            *reinterpret_cast<f32x4 *>(mine + 16 * __lane_id() + 4 * v) =
+                f32x4{acc[g][4 * v], acc[g][4 * v + 1], acc[g][4 * v + 2], acc[g][4 * v + 3]};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int e = 256 * v + 4 * __lane_id();
+            const f32x4 x = *reinterpret_cast<const f32x4 *>(mine + e);
+            if (1024 * g + e < wt.lenpad)
+                *reinterpret_cast<f32x4 *>(out + wt.t.dst + 1024 * g + e) = x;
+        }
     }
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-        *reinterpret_cast<f32x4 *>(mine + 16 * __lane_id() + 4 * v) =
-            f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const int e = 256 * v + 4 * __lane_id();
-        const f32x4 x = *reinterpret_cast<const f32x4 *>(mine + e);
-        if (e < wt.lenpad) *reinterpret_cast<f32x4 *>(out + wt.t.dst + e) = x;
-    }
-#elif DLS_QUANT_STORE == 1
-    if (!wt.active) return;
-    if (wt.e0 + 16 > wt.t.len) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = (wt.e0 + e < wt.t.len) ? acc[e] : 0.f;
-    }
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-        __builtin_nontemporal_store(f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]},
-                                    reinterpret_cast<f32x4 *>(out + wt.t.dst + wt.e0) + v);
-#else
-    store16(wt, acc, out);
+}
+
+#ifndef DLS_QUANT_MINB
+#define DLS_QUANT_MINB 1
 #endif
+template <int G>
+__global__ __launch_bounds__(kBlock, DLS_QUANT_MINB) void k_dequant_fast(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
+    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
+    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
+    // one launch per slice count G: each instance has its own register budget
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    if (wt.t.kind == 1)
+        fast_tile<true, G>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+    else
+        fast_tile<false, G>(wt, Q, ldq, sz, L, rows, w, K, d, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
@@ -690,16 +727,21 @@ __global__ __launch_bounds__(kBlock) void k_quantize(const float *__restrict__ x
 
 using namespace dls;
 
-extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_t nfast,
+extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast,
                                   const void *Q, int64_t ldq, const float *F, int64_t ldf,
                                   const float *sz, int64_t sz_row, int64_t sz_chan,
                                   const int32_t *rows,
                                   const float *weight, int32_t K, float total, float *out,
                                   dls_stream_t stream) {
-    DLS_REQUIRE(tiles && rows && weight && out && sz, DLS_EINVAL,
+    DLS_REQUIRE(tiles && nfast && rows && weight && out && sz, DLS_EINVAL,
                 "dls_dequant_fedavg: null pointer");
-    DLS_REQUIRE(ntiles > 0 && K > 0 && nfast >= 0 && nfast <= ntiles, DLS_EINVAL,
-                "dls_dequant_fedavg: ntiles=%d nfast=%d K=%d", ntiles, nfast, K);
+    int64_t nf = 0;
+    for (int g = 0; g < 4; ++g) {
+        DLS_REQUIRE(nfast[g] >= 0, DLS_EINVAL, "dls_dequant_fedavg: nfast[%d]=%d", g, nfast[g]);
+        nf += nfast[g];
+    }
+    DLS_REQUIRE(ntiles > 0 && K > 0 && nf <= ntiles, DLS_EINVAL,
+                "dls_dequant_fedavg: ntiles=%d fast tiles=%lld K=%d", ntiles, (long long)nf, K);
     DLS_REQUIRE(ldq % 16 == 0 && ldf % 4 == 0 && aligned16(out) && (!Q || aligned16(Q)) &&
                     (!F || aligned16(F)),
                 DLS_ELAYOUT, "dls_dequant_fedavg: ldq %% 16, ldf %% 4, 16-byte alignment");
@@ -710,14 +752,26 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
-    if (nfast > 0)
-        hipLaunchKernelGGL(k_dequant_fast, dim3((unsigned)((nfast + wpb - 1) / wpb)), dim3(kBlock),
-                           0, st, tiles, (int)nfast, reinterpret_cast<const uint8_t *>(Q), ldq,
-                           reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
-    const int ngen = ntiles - nfast;
+    const dls_qtile *t = tiles;
+    for (int g = 0; g < 4; ++g) {  // groups of 4, 3, 2, 1 slices
+        const int n = nfast[g];
+        if (n == 0) continue;
+        const dim3 grid((unsigned)((n + wpb - 1) / wpb));
+#define DLS_FAST_LAUNCH(G_)                                                                       \
+    hipLaunchKernelGGL(k_dequant_fast<G_>, grid, dim3(kBlock), 0, st, t, n,                       \
+                       reinterpret_cast<const uint8_t *>(Q), ldq, reinterpret_cast<const f32x2 *>(sz), \
+                       L, rows, weight, (int)K, d, out)
+        if (g == 0) DLS_FAST_LAUNCH(4);
+        else if (g == 1) DLS_FAST_LAUNCH(3);
+        else if (g == 2) DLS_FAST_LAUNCH(2);
+        else DLS_FAST_LAUNCH(1);
+#undef DLS_FAST_LAUNCH
+        t += n;
+    }
+    const int ngen = ntiles - (int)nf;
     if (ngen > 0)
         hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
-                           dim3(kBlock), 0, st, tiles + nfast, ngen,
+                           dim3(kBlock), 0, st, t, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
     return check_launch("dls_dequant_fedavg");

@@ -14,10 +14,11 @@ HBM layout per client row:
   sz fp32  [C+1, capacity, 2] (fl32(scale), zero_point) per output channel,
                              channel-major: a wave's per-channel table load for 64
                              clients reads 512 consecutive bytes
-and a tile table (``dls_qtile``) built once per layout: wave tiles of <= 1024
-elements inside one tensor, which also carry the channel bookkeeping; the
-tiles whose elements all lie in one output channel come first (``nfast``) and
-run on the streamlined kernel.
+and a tile table (``dls_qtile``) built once per layout: wave tiles inside one
+tensor, which also carry the channel bookkeeping; the tiles whose elements all
+lie in one output channel (<= 4096 elements) come first, grouped by 1 KiB slice
+count (``nfast``), and run on the streamlined kernels, the rest (<= 1024
+elements) on the general one.
 """
 import numpy as np
 import torch
@@ -25,7 +26,8 @@ import torch
 from . import _native
 from .layout import ALIGN, ParameterLayout, _round_up
 
-TILE = 1024  # one wavefront: 64 lanes x 16 elements
+TILE = 1024  # one wavefront slice: 64 lanes x 16 elements
+FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
 QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
 
 QTILE_DTYPE = np.dtype([("dst", "<i8"), ("src", "<i8"), ("len", "<i4"), ("kind", "<i4"),
@@ -95,24 +97,42 @@ class QuantLayout:
         return True
 
     def tiles(self):
-        """(table, nfast): wave tiles, one-channel int tiles first."""
+        """(table, nfast): wave tiles, one-channel int tiles first, grouped by their
+        number of 1 KiB slices (nfast = their counts for 4, 3, 2, 1 slices).
+
+        int tensors whose channel rows are long (>= 1024, multiple of 64) and
+        fill 1 KiB slices well get channel-aligned tiles of up to FAST_TILE
+        elements (a wave streams up to 4 KiB of every client row); every other
+        tensor is cut into TILE-element tiles from its start."""
         rows = []
         for i, kind in enumerate(self.kinds):
             n = self.layout.numels[i]
+            rl = self.row_len[i]
+            off, src, cb = self.layout.offsets[i], self.src[i], self.chan_base[i]
+            cend = cb + self.channels[i] if kind else 0
+            waste = -rl % TILE  # idle lanes of the row's last slice
+            if kind and rl >= TILE and rl % 64 == 0 and 8 * waste <= rl:
+                for c in range(self.channels[i]):
+                    for j in range(0, rl, FAST_TILE):
+                        e = c * rl + j
+                        rows.append((off + e, src + e, min(FAST_TILE, rl - j), kind, cb + c, rl,
+                                     j, cend))
+                continue
             for e in range(0, n, TILE):
-                ln = min(TILE, n - e)
-                rl = self.row_len[i]
-                rows.append((self.layout.offsets[i] + e, self.src[i] + e, ln, kind,
-                             self.chan_base[i] + e // rl if kind else 0, rl,
-                             e % rl if kind else 0,
-                             self.chan_base[i] + self.channels[i] if kind else 0))
+                rows.append((off + e, src + e, min(TILE, n - e), kind, cb + e // rl if kind else 0,
+                             rl, e % rl if kind else 0, cend))
 
         def one_channel(r):
             return r[3] != 0 and r[6] + r[2] <= r[5]  # kind int, row_pos + len <= row_len
 
-        fast = [r for r in rows if one_channel(r)]
+        def slices(r):
+            return (r[2] + 63) // 64 * 64 // TILE + ((r[2] + 63) // 64 * 64 % TILE != 0)
+
+        fast = [[r for r in rows if one_channel(r) and slices(r) == g] for g in (4, 3, 2, 1)]
         rest = [r for r in rows if not one_channel(r)]
-        return np.array(fast + rest, dtype=QTILE_DTYPE), len(fast)
+        assert all(r[2] <= TILE for r in rest)
+        return (np.array([r for grp in fast for r in grp] + rest, dtype=QTILE_DTYPE),
+                tuple(len(grp) for grp in fast))
 
 
 class QuantizedClientStore:

@@ -135,13 +135,15 @@ int dls_sign_sgd_apply(float *param, const uint64_t *vote_planes, int64_t P, flo
  * Wave tile of the flattened parameter space for the fused dequant-FedAvg
  * kernels.  A tile lies inside one tensor; host code builds the table once per
  * layout, with the "fast" tiles first: int tiles (kind 1/2) whose real
- * elements all lie in channel chan0. */
+ * elements all lie in channel chan0, grouped by 1 KiB slice count. */
 typedef struct dls_qtile {
     int64_t dst;     /* first output element (flat layout offset, multiple of 16) */
     int64_t src;     /* first element within a client row of Q (kind 1/2) or F (kind 0) */
-    int32_t len;     /* elements, <= 1024; lanes cover 16-element chunks up to the
-                        next multiple of 64 (the rows are padded to 64) and write
-                        0 past len, so the output's row padding is always zero */
+    int32_t len;     /* elements: <= 4096 for the fast tiles, <= 1024 for the rest;
+                        lanes cover 16-element chunks (lane l, KiB slice g: element
+                        1024 g + 16 l) up to the next multiple of 64 (the rows are
+                        padded to 64) and write 0 past len, so the output's row
+                        padding is always zero */
     int32_t kind;    /* 0 = fp32 tensor, 1 = int8 per-channel, 2 = uint8 per-channel */
     int32_t chan0;   /* channel (index into the client's scale/zp row) of element 0 */
     int32_t row_len; /* elements per output channel */
@@ -155,9 +157,12 @@ typedef struct dls_qtile {
  *   out[e] (+)= fl(fl(x * n_i) / N)                              (fp32 tensors)
  * bit-exact in client order.  Q int8/uint8 [*, ldq], F fp32 [*, ldf],
  * sz fp32 pairs (fl32(scale), zero_point): client row r, channel c at pair
- * r * sz_row + c * sz_chan (the store keeps them channel-major: sz_row = 1).  Tiles
- * [0, nfast) must be one-channel int tiles (see dls_qtile). */
-int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, int32_t nfast, const void *Q,
+ * r * sz_row + c * sz_chan (the store keeps them channel-major: sz_row = 1).
+ * nfast: host array of 4 counts; the table starts with nfast[0] one-channel int
+ * tiles of 4 KiB slices (3072 < len <= 4096), then nfast[1] of 3, nfast[2] of 2
+ * and nfast[3] of 1 (len <= 1024); the remaining tiles (len <= 1024) may be of
+ * any kind (see dls_qtile). */
+int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast, const void *Q,
                        int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t sz_row,
                        int64_t sz_chan, const int32_t *rows, const float *weight, int32_t K,
                        float total, float *out, dls_stream_t stream);

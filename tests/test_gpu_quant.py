@@ -170,14 +170,18 @@ def test_stochastic_quantize_unbiased():
     assert abs(float(deq.mean()) - 0.3) < 1e-3
 
 
-@pytest.mark.parametrize("K", [1, 63, 64, 65, 130])
-def test_dequant_fedavg_chunked_clients_one_channel(K):
+@pytest.mark.parametrize("K,L", [(1, 2500), (63, 2500), (64, 2500), (65, 2500), (130, 2500),
+                                 (65, 11264), (3, 6144), (17, 3072), (9, 5120), (64, 1024),
+                                 (130, 4160)])
+def test_dequant_fedavg_chunked_clients_one_channel(K, L):
     """K across the kernels' 64-client chunks; long channel rows (one-channel
-    tiles), int8 symmetric, uint8 with zero points for which fl(zp*s) is and is
-    not exact, and a channel whose scale forces the IEEE-division path."""
+    tiles: 1 KiB tiles from the tensor start for L = 2500 / 4160, channel-aligned
+    tiles of 4, 3, 2 and 1 KiB slices for the other L), int8 symmetric, uint8 with
+    zero points for which fl(zp*s) is and is not exact, and a channel whose scale
+    forces the IEEE-division path."""
     from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
-    g = torch.Generator().manual_seed(K)
-    C, L = 5, 2500
+    g = torch.Generator().manual_seed(K * 7 + L)
+    C = 5
     payloads, n = [], []
     for k in range(K):
         s8 = torch.rand(C, generator=g, dtype=torch.float64) * 1e-2 + 1e-4
@@ -198,7 +202,9 @@ def test_dequant_fedavg_chunked_clients_one_channel(K):
         r = store.acquire()
         store.write(r, p)
         rows.append(r)
-    assert store.nfast > 0
+    assert sum(store.nfast) > 0
+    if L % 1024 == 0 or L in (5120, 11264):
+        assert store.nfast[4 - -(-min(L, 4096) // 1024)] > 0  # the widest slice group is used
     order = list(torch.randperm(K, generator=g).tolist())
     out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order]))
     layout = [("a", (C, L)), ("b", (C, L)), ("bias", (C,))]

@@ -49,15 +49,46 @@ def test_quant_layout_tiles():
     assert t["len"].max() <= 1024 and all(d % 16 == 0 for d in t["dst"])
     # one-channel int tiles first: the 15 tiles of the 3x5000 "u" are one-channel
     # except those starting at 4096 and 9216, which cross a row boundary
-    fast, rest = t[:nfast], t[nfast:]
+    nf = sum(nfast)
+    fast, rest = t[:nf], t[nf:]
     assert all(r["kind"] != 0 and r["row_pos"] + r["len"] <= r["row_len"] for r in fast)
     assert all(r["kind"] == 0 or r["row_pos"] + r["len"] > r["row_len"] for r in rest)
     assert sorted(rest["kind"].tolist()) == [0, 1, 2, 2]
-    assert nfast == 13 and sum(int(r["len"]) for r in t) == 45 + 5 + 15000
+    assert nfast == (0, 0, 0, 13) and sum(int(r["len"]) for r in t) == 45 + 5 + 15000
     u = t[t["kind"] == 2]
     assert all(int(r["row_pos"]) == int(r["src"] - ql.src[2]) % 5000 for r in u)
     assert all(int(r["chan0"]) == 5 + int(r["src"] - ql.src[2]) // 5000 for r in u)
     assert ql.matches(payload)
+
+
+def test_quant_layout_channel_aligned_tiles():
+    """Long channel rows (multiple of 64, last 1 KiB slice at least 7/8 full) get
+    channel-aligned tiles of up to 4096 elements, grouped by slice count."""
+    from distributed_learning_simulator_amd.quant_store import QuantLayout
+    shapes = {"fc": (3, 25088), "conv": (2, 512, 3, 3), "mid": (4, 256, 3, 3), "k": (2, 1024)}
+    payload = {k: (torch.zeros(s, dtype=torch.int8), torch.ones(s[0]), torch.zeros(s[0]))
+               for k, s in shapes.items()}
+    ql = QuantLayout(payload)
+    t, nfast = ql.tiles()
+    # fc: 6 x 4096 + 512 per channel; conv (row 4608): 4096 + 512; k: 1024;
+    # mid (row 2304: 768 idle lanes in its last slice) keeps 1 KiB tiles from its start
+    assert nfast == (3 * 6 + 2, 0, 0, 3 + 2 + 2 + 6)  # 6 of mid's 9 tiles lie in one channel
+    nf = sum(nfast)
+    sl = [(int(r["len"]) + 1023) // 1024 for r in t[:nf]]
+    assert sl == sorted(sl, reverse=True)
+    assert all(r["row_pos"] + r["len"] <= r["row_len"] for r in t[:nf])
+    assert all(d % 16 == 0 for d in t["dst"]) and all(s % 16 == 0 for s in t["src"])
+    assert t["len"][nf:].max() <= 1024
+    for i, name in enumerate(ql.names):  # every element of every tensor exactly once
+        mine = t[(t["dst"] >= ql.layout.offsets[i]) &
+                 (t["dst"] < ql.layout.offsets[i] + ql.layout.numels[i])]
+        cover = np.zeros(ql.layout.numels[i], np.int32)
+        for r in mine:
+            e = int(r["dst"]) - ql.layout.offsets[i]
+            cover[e:e + int(r["len"])] += 1
+            assert int(r["src"]) - ql.src[i] == e
+            assert int(r["chan0"]) == ql.chan_base[i] + e // ql.row_len[i]
+        assert (cover == 1).all(), name
 
 
 def test_repeated_result_served_once_per_consumer():

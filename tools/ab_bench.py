@@ -15,6 +15,7 @@ import os
 import statistics
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -29,11 +30,20 @@ P_ = ctypes.c_void_p
 
 def load(path):
     L = ctypes.CDLL(path)
+    # libraries named libdls_old*.so predate nfast[4] (they take the fast-tile total)
+    L.old_nfast = os.path.basename(path).startswith("libdls_old")
     for name, (args, res) in _native.SIGNATURES.items():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    if L.old_nfast:
+        L.dls_dequant_fedavg.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32] + \
+            L.dls_dequant_fedavg.argtypes[3:]
     return L
+
+
+def nfast_arg(L, counts):
+    return int(sum(counts)) if L.old_nfast else (ctypes.c_int32 * 4)(*counts)
 
 
 def ptr(t):
@@ -94,14 +104,27 @@ def setup(dev, want=()):
     ql = st.qlayout
     Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
     Pf = sum(m for m, k in zip(st.layout.numels, ql.kinds) if not k)
-    W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, st.nfast, ptr(st.Q), st.Q.stride(0),
+    W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast), ptr(st.Q), st.Q.stride(0),
                                                  ptr(st.F), st.F.stride(0), ptr(st.sz),
                                                  st.sz.stride(1) // 2, st.sz.stride(0) // 2,
                                                  ptr(rows), ptr(w), 100, tot,
                                                  ptr(qo), stream()),
                   100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+    # the same payloads with 1 KiB tiles only (FAST_TILE = TILE): the single-slice
+    # kernel path, and the only tiling a library from before multi-KiB tiles handles
+    from distributed_learning_simulator_amd import quant_store as qs
+    saved, qs.FAST_TILE = qs.FAST_TILE, qs.TILE
+    t1, nf1 = ql.tiles()
+    qs.FAST_TILE = saved
+    tiles1 = torch.from_numpy(t1.view(np.uint8).copy()).to(dev)
+    W["quant1k"] = (lambda L: L.dls_dequant_fedavg(ptr(tiles1), len(t1), nfast_arg(L, nf1), ptr(st.Q),
+                                                   st.Q.stride(0), ptr(st.F), st.F.stride(0),
+                                                   ptr(st.sz), st.sz.stride(1) // 2,
+                                                   st.sz.stride(0) // 2, ptr(rows), ptr(w), 100,
+                                                   tot, ptr(qo), stream()),
+                    100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
     rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
-    W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, st.nfast,
+    W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast),
                                                          ptr(st.Q), st.Q.stride(0),
                                                          ptr(st.F), st.F.stride(0), ptr(st.sz),
                                                          st.sz.stride(1) // 2,

@@ -21,7 +21,7 @@ def build(name, defs, src=CSRC):
     objs = []
     for s in SRCS:
         o = os.path.join(d, s.replace(".hip", ".o"))
-        subprocess.check_call(["hipcc", *FLAGS, *defs, "-I", CSRC, "-c", os.path.join(src, s), "-o", o])
+        subprocess.check_call(["hipcc", *FLAGS, *defs, "-I", src, "-c", os.path.join(src, s), "-o", o])
         objs.append(o)
     lib = os.path.join(OUT, f"libdls_{name}.so")
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, *objs])
@@ -36,12 +36,18 @@ def main(specs):
         name, _, flags = spec.partition(":")
         src = CSRC
         if rev:
-            src = os.path.join(OUT, f"_src_{rev}")
+            # <tree>/pkg/csrc + <tree>/include: dls_common.h's "../../include/dls_hip.h"
+            # resolves to the revision's own header
+            tree = os.path.join(OUT, f"_src_{rev}")
+            src = os.path.join(tree, "pkg", "csrc")
             os.makedirs(src, exist_ok=True)
+            os.makedirs(os.path.join(tree, "include"), exist_ok=True)
             for f in SRCS + ["dls_common.h"]:
                 blob = subprocess.check_output(
                     ["git", "-C", ROOT, "show", f"{rev}:distributed_learning_simulator_amd/csrc/{f}"])
                 open(os.path.join(src, f), "wb").write(blob)
+            blob = subprocess.check_output(["git", "-C", ROOT, "show", f"{rev}:include/dls_hip.h"])
+            open(os.path.join(tree, "include", "dls_hip.h"), "wb").write(blob)
         jobs.append((name, [f for f in flags.split(",") if f], src))
     with cf.ThreadPoolExecutor(4) as ex:
         for lib in ex.map(lambda j: build(*j), jobs):
