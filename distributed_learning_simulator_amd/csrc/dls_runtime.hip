@@ -58,6 +58,23 @@ int resident_blocks(const void *kernel, int block, size_t lds) {
     return n;
 }
 
+hipStream_t side_stream() {
+    // one non-blocking stream per device, created on first use and kept for the
+    // process (the library's launchers fork small concurrent kernels onto it and
+    // join back to the caller's stream before returning)
+    static std::mutex mu;
+    static std::unordered_map<int, hipStream_t> streams;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = streams.find(dev);
+    if (it != streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[dev] = s;
+    return s;
+}
+
 }  // namespace dls
 
 extern "C" {

@@ -2,7 +2,7 @@
 //
 // One pass over the client rows: each lane owns 4 consecutive parameters per
 // 1 KB slice of a row (one 16-byte load per client; a wave owns 1 slice, or 16
-// consecutive slices on large models), walks the K clients in the reference's
+// or 22 consecutive slices on large models), walks the K clients in the reference's
 // iteration order and keeps the running sum in registers, so every client byte
 // is read once and the 4*P-byte result is written once.  HBM-bound: the
 // algorithmic traffic of one call is K*P*4 + P*4 bytes.  The client rows and
@@ -228,16 +228,29 @@ extern "C" int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows,
     hipStream_t st = as_stream(stream);
     if (mode == DLS_FEDAVG_EXACT) {
         const FastDiv d = make_fastdiv(total);
-        // large models: each wave streams 16 KB of every client row (one client
-        // per double-buffered step; measured 4-5 % faster than 1 KB x 4 clients
-        // at P = 11.2M) while the grid still holds >= 1024 waves
-        const int64_t wide_waves = (P4 + 64 * 16 - 1) / (64 * 16);
+        // large models: each wave streams G KB of every client row (one client per
+        // double-buffered step; 1 KB x 4 clients per wave was 4-6 % slower at
+        // P = 11.2M).  G = 22 or 16, whichever leaves the last generation of
+        // resident waves fuller (a nearly empty last generation cost 13 % for
+        // G = 14 at P = 11.2M; 22 is 1.7 % faster than 16 there); the grid must
+        // hold at least one full generation.
         const f32x4 *Uv = reinterpret_cast<const f32x4 *>(U);
         f32x4 *ov = reinterpret_cast<f32x4 *>(out);
-        if (wide_waves >= 1024)
-            hipLaunchKernelGGL((k_fedavg_exact_pipe<1, true, 16>),
-                               dim3((unsigned)((wide_waves + 3) / 4)), dim3(kPipeBlock), 0, st, Uv,
-                               ldu / 4, rows, weight, (int)K, d, P4, ov);
+        auto fill = [&](const void *kern, int G, int64_t &waves) {
+            waves = (P4 + 64 * G - 1) / (64 * G);
+            const int64_t slots = (int64_t)resident_blocks(kern, kPipeBlock, 0) * (kPipeBlock / 64);
+            if (waves < slots) return -1.0;
+            return (double)waves / (double)(((waves + slots - 1) / slots) * slots);
+        };
+        int64_t w22 = 0, w16 = 0;
+        const double e22 = fill(reinterpret_cast<const void *>(k_fedavg_exact_pipe<1, true, 22>), 22, w22);
+        const double e16 = fill(reinterpret_cast<const void *>(k_fedavg_exact_pipe<1, true, 16>), 16, w16);
+        if (e22 > 0 && e22 >= e16)
+            hipLaunchKernelGGL((k_fedavg_exact_pipe<1, true, 22>), dim3((unsigned)((w22 + 3) / 4)),
+                               dim3(kPipeBlock), 0, st, Uv, ldu / 4, rows, weight, (int)K, d, P4, ov);
+        else if (e16 > 0)
+            hipLaunchKernelGGL((k_fedavg_exact_pipe<1, true, 16>), dim3((unsigned)((w16 + 3) / 4)),
+                               dim3(kPipeBlock), 0, st, Uv, ldu / 4, rows, weight, (int)K, d, P4, ov);
         else
             hipLaunchKernelGGL((k_fedavg_exact_pipe<4, true, 1>),
                                dim3((unsigned)((P4 + kPipeBlock - 1) / kPipeBlock)),

@@ -22,6 +22,9 @@ constexpr int kBlock = 256;
 #ifndef DLS_QUANT_UG
 #define DLS_QUANT_UG 1  // clients per batch on multi-KiB tiles
 #endif
+#ifndef DLS_QUANT_FORK
+#define DLS_QUANT_FORK 1  // small tile groups on a side stream: 0 off, 1 before the bulk, 2 after
+#endif
 #ifndef DLS_QUANT_SCHED
 #define DLS_QUANT_SCHED 2  // element pairs between scheduling barriers (0: none)
 #endif
@@ -752,13 +755,35 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
+    // The widest non-empty group carries the bulk of the bytes; the other groups
+    // and the general tiles are small grids whose waves are latency-bound
+    // (100+ dependent client steps each), so they run on a side stream,
+    // concurrently with the bulk kernel, and the caller's stream joins them.
+    const dls_qtile *tg[4];
     const dls_qtile *t = tiles;
-    for (int g = 0; g < 4; ++g) {  // groups of 4, 3, 2, 1 slices
+    int big = -1;
+    for (int g = 0; g < 4; ++g) {
+        tg[g] = t;
+        t += nfast[g];
+        if (big < 0 && nfast[g] > 0) big = g;
+    }
+    const int ngen = ntiles - (int)nf;
+    const int64_t small_tiles = nf - (big >= 0 ? nfast[big] : 0) + ngen;
+    hipStream_t side = st;
+    hipEvent_t fork = nullptr, join = nullptr;
+    if (DLS_QUANT_FORK && big >= 0 && small_tiles > 0) {
+        hipStream_t s2 = side_stream();
+        if (s2 && hipEventCreateWithFlags(&fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&join, hipEventDisableTiming) == hipSuccess &&
+            hipEventRecord(fork, st) == hipSuccess && hipStreamWaitEvent(s2, fork, 0) == hipSuccess)
+            side = s2;
+    }
+    auto launch_fast = [&](int g, hipStream_t s) {
         const int n = nfast[g];
-        if (n == 0) continue;
+        if (n == 0) return;
         const dim3 grid((unsigned)((n + wpb - 1) / wpb));
 #define DLS_FAST_LAUNCH(G_)                                                                       \
-    hipLaunchKernelGGL(k_dequant_fast<G_>, grid, dim3(kBlock), 0, st, t, n,                       \
+    hipLaunchKernelGGL(k_dequant_fast<G_>, grid, dim3(kBlock), 0, s, tg[g], n,                    \
                        reinterpret_cast<const uint8_t *>(Q), ldq, reinterpret_cast<const f32x2 *>(sz), \
                        L, rows, weight, (int)K, d, out)
         if (g == 0) DLS_FAST_LAUNCH(4);
@@ -766,15 +791,29 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
         else if (g == 2) DLS_FAST_LAUNCH(2);
         else DLS_FAST_LAUNCH(1);
 #undef DLS_FAST_LAUNCH
-        t += n;
-    }
-    const int ngen = ntiles - (int)nf;
+    };
+    if (DLS_QUANT_FORK == 2 && big >= 0) launch_fast(big, st);
+    for (int g = 0; g < 4; ++g)
+        if (g != big) launch_fast(g, side);
     if (ngen > 0)
         hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
-                           dim3(kBlock), 0, st, t, ngen,
+                           dim3(kBlock), 0, side, t, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
-    return check_launch("dls_dequant_fedavg");
+    if (DLS_QUANT_FORK != 2 && big >= 0) launch_fast(big, st);
+    int rc = check_launch("dls_dequant_fedavg");
+    if (side != st) {
+        hipError_t e = hipEventRecord(join, side);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, join, 0);
+        if (e != hipSuccess) {  // the caller's stream must not run ahead of the side work
+            (void)hipStreamSynchronize(side);
+            set_error("dls_dequant_fedavg: stream join failed: %s", hipGetErrorString(e));
+            rc = (int)e;
+        }
+    }
+    if (fork) (void)hipEventDestroy(fork);  // released once the enqueued record / wait complete
+    if (join) (void)hipEventDestroy(join);
+    return rc;
 }
 
 extern "C" int dls_segment_minmax_f32(const float *x, const int64_t *seg_off, int32_t nseg,

@@ -30,8 +30,8 @@ P_ = ctypes.c_void_p
 
 def load(path):
     L = ctypes.CDLL(path)
-    # libraries named libdls_old*.so predate nfast[4] (they take the fast-tile total)
-    L.old_nfast = os.path.basename(path).startswith("libdls_old")
+    # libraries named libdls_oldabi*.so predate nfast[4] (they take the fast-tile total)
+    L.old_nfast = os.path.basename(path).startswith("libdls_oldabi")
     for name, (args, res) in _native.SIGNATURES.items():
         f = getattr(L, name)
         f.argtypes = args
@@ -114,10 +114,10 @@ def setup(dev, want=()):
     # kernel path, and the only tiling a library from before multi-KiB tiles handles
     from distributed_learning_simulator_amd import quant_store as qs
     saved, qs.FAST_TILE = qs.FAST_TILE, qs.TILE
-    t1, nf1 = ql.tiles()
+    qt1, nf1 = ql.tiles()
     qs.FAST_TILE = saved
-    tiles1 = torch.from_numpy(t1.view(np.uint8).copy()).to(dev)
-    W["quant1k"] = (lambda L: L.dls_dequant_fedavg(ptr(tiles1), len(t1), nfast_arg(L, nf1), ptr(st.Q),
+    tiles1 = torch.from_numpy(qt1.view(np.uint8).copy()).to(dev)
+    W["quant1k"] = (lambda L: L.dls_dequant_fedavg(ptr(tiles1), len(qt1), nfast_arg(L, nf1), ptr(st.Q),
                                                    st.Q.stride(0), ptr(st.F), st.F.stride(0),
                                                    ptr(st.sz), st.sz.stride(1) // 2,
                                                    st.sz.stride(0) // 2, ptr(rows), ptr(w), 100,

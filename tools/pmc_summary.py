@@ -29,11 +29,12 @@ WORKLOADS = {  # workload -> [(kernel regexes summed per launch, key in pmc_traf
 
 
 def values(path, counter, kernel):
-    out = []
+    """{full kernel name (one template instance): [value per launch]}"""
+    out = {}
     with open(path) as f:
         for row in csv.DictReader(f):
             if row["Counter_Name"] == counter and re.search(r"\b" + kernel + r"(\b|<)", row["Kernel_Name"]):
-                out.append(float(row["Counter_Value"]))
+                out.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
     return out
 
 
@@ -51,10 +52,11 @@ def main(tag):
                                             "run_counter_collection.csv"), "FETCH_SIZE", name)
                     w = values(os.path.join(base, f"pmc_{wl}_WRITE_SIZE",
                                             "run_counter_collection.csv"), "WRITE_SIZE", name)
-                    if f and w:
-                        fm += statistics.median(f)
-                        wm += statistics.median(w)
-                        nl = max(nl, len(f))
+                    # every instance (e.g. k_dequant_fast<4..1>) runs once per call
+                    for inst in f.keys() & w.keys():
+                        fm += statistics.median(f[inst])
+                        wm += statistics.median(w[inst])
+                        nl = max(nl, len(f[inst]))
             except OSError:
                 continue
             if not nl:
