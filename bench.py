@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 from distributed_learning_simulator_amd import _native  # noqa: E402
 from distributed_learning_simulator_amd.layout import ParameterLayout  # noqa: E402
+from distributed_learning_simulator_amd.distributed import chunk_bounds  # noqa: E402
 from distributed_learning_simulator_amd.model_shapes import resnet18_cifar, vgg16  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -122,7 +123,7 @@ def bench_fedavg(args, dev, rank, world):
     w = torch.tensor(n, dtype=torch.float32, device=dev)
     out = torch.empty(P, dtype=torch.float32, device=dev)
     chunks = args.chunks if world > 1 else 1
-    bounds = [P * c // chunks // 256 * 256 for c in range(chunks)] + [P]
+    bounds = chunk_bounds(P, chunks)  # decreasing sizes: the exposed last all-reduce is small
     kms = []
 
     def step(a=None, b=None):

@@ -67,18 +67,22 @@ class ClientUpdateStore:
         return self.layout.views(self.U[row])
 
     # ------------------------------------------------------------ aggregation
-    def fedavg(self, rows, ns, mode=_native.FEDAVG_EXACT, out=None, total=None):
+    def fedavg(self, rows, ns, mode=_native.FEDAVG_EXACT, out=None, total=None, cols=None):
         """Weighted mean of rows in the given order (servers/fed_server.py:44-66).
 
         ``total`` (default: sum of ``ns``) is the divisor N; a shard of a sharded
-        round passes the global N and gets its partial sum."""
-        P = self.layout.P
+        round passes the global N and gets its partial sum.  ``cols = (c0, c1)``
+        (multiples of 4) reduces only flat elements [c0, c1) into ``out`` (of that
+        length); rows / ns may then be device int32 / fp32 tensors, reused across
+        column ranges."""
+        c0, c1 = cols if cols is not None else (0, self.layout.P)
         if out is None:
-            out = torch.empty(P, dtype=torch.float32, device=self.device)
+            out = torch.empty(c1 - c0, dtype=torch.float32, device=self.device)
         if total is None:
             total = sum(int(n) for n in ns)
-        _native.fedavg(self.U, _i32(rows, self.device), _f32([int(n) for n in ns], self.device),
-                       float(total), P, out, mode=mode)
+        r = rows if torch.is_tensor(rows) else _i32(rows, self.device)
+        w = ns if torch.is_tensor(ns) else _f32([int(n) for n in ns], self.device)
+        _native.fedavg(self.U[:, c0:], r, w, float(total), c1 - c0, out, mode=mode)
         return out
 
     def subset_models(self, subsets, n_of_row, method="exact", out=None):

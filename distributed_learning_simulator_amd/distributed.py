@@ -52,14 +52,27 @@ def global_sample_count(local_ns, device, group=None):
     return int(t.item())
 
 
+def chunk_bounds(P, chunks):
+    """Element bounds of ``chunks`` pieces of a P-element vector, multiples of 256,
+    sizes decreasing linearly (weights chunks, chunks-1, ..., 1): only the last
+    piece's all-reduce runs after the last reduction kernel, so it is the small one."""
+    tot = chunks * (chunks + 1) // 2
+    acc, bounds = 0, [0]
+    for c in range(chunks - 1):
+        acc += chunks - c
+        bounds.append(min(P, P * acc // tot // 256 * 256))
+    bounds.append(P)
+    return bounds
+
+
 def allreduce_chunked(flat, chunks=4, group=None, produce=None):
-    """SUM all-reduce of a flat fp32 vector in ``chunks`` pieces.
+    """SUM all-reduce of a flat fp32 vector in ``chunks`` pieces (chunk_bounds).
 
     ``produce(c0, c1)`` (optional) fills flat[c0:c1] first; chunk c's all-reduce
     is issued asynchronously before chunk c+1 is produced, so RCCL over xGMI
     overlaps the next chunk's reduction kernel."""
     P = flat.numel()
-    bounds = [P * c // chunks // 256 * 256 for c in range(chunks)] + [P]
+    bounds = chunk_bounds(P, chunks)
     handles = []
     for c in range(chunks):
         c0, c1 = bounds[c], bounds[c + 1]
@@ -105,16 +118,17 @@ class ShardedFedServer(_ShardedMixin, FedServer):
         store = self.parameters.store
         rows = [self.parameters.row_of(i) for i in ids]
         out = torch.zeros(store.layout.P, dtype=torch.float32, device=self.device)
+        produce = None
         if rows:
-            self._aggregate(store, rows, ns, total=total, out=out)
-        allreduce_chunked(out, self.chunks, self.group)
-        return store.layout.views(out)
+            from .aggregation import _f32, _i32
+            from .servers.fed_server import _MODES
+            r, w = _i32(rows, self.device), _f32(ns, self.device)
+            mode = _MODES[self.aggregation_mode]
 
-    def _aggregate(self, store, rows, ns, total=None, out=None):
-        if out is None:
-            return super()._aggregate(store, rows, ns, total)
-        from .servers.fed_server import _MODES
-        return store.fedavg(rows, ns, mode=_MODES[self.aggregation_mode], total=total, out=out)
+            def produce(c0, c1):  # reduce chunk c while chunk c-1 is on the wire
+                store.fedavg(r, w, mode=mode, total=total, out=out[c0:c1], cols=(c0, c1))
+        allreduce_chunked(out, self.chunks, self.group, produce=produce)
+        return store.layout.views(out)
 
 
 class ShardedFedQuantServer(_ShardedMixin, FedQuantServer):
