@@ -228,34 +228,40 @@ extern "C" int dls_fedavg_f32(const float *U, int64_t ldu, const int32_t *rows,
     hipStream_t st = as_stream(stream);
     if (mode == DLS_FEDAVG_EXACT) {
         const FastDiv d = make_fastdiv(total);
-        // large models: each wave streams G KB of every client row (one client per
-        // double-buffered step; 1 KB x 4 clients per wave was 4-6 % slower at
-        // P = 11.2M).  G = 22 or 16, whichever leaves the last generation of
-        // resident waves fuller (a nearly empty last generation cost 13 % for
-        // G = 14 at P = 11.2M; 22 is 1.7 % faster than 16 there); the grid must
-        // hold at least one full generation.
+        // Each wave streams G KB of every client row (one client per double-
+        // buffered step); wide G beats 1 KB x 4 clients by 4-6 % at P = 11.2M.
+        // A wave's work is K clients deep, so the grid is cut into pieces of at
+        // most one generation of resident waves, launched back to back: a
+        // second generation starting piecemeal behind the first, or a last
+        // generation of a few waves running alone at latency-bound speed, costs
+        // more than a kernel boundary (measured: G = 14 at P = 11.2M leaves 46
+        // waves for a 4th generation, +13 %; two one-generation launches beat one
+        // two-generation launch by 3 %).  Widest G that keeps >= kSat waves per
+        // piece; the 1 KB kernel for small models.
         const f32x4 *Uv = reinterpret_cast<const f32x4 *>(U);
         f32x4 *ov = reinterpret_cast<f32x4 *>(out);
-        auto fill = [&](const void *kern, int G, int64_t &waves) {
-            waves = (P4 + 64 * G - 1) / (64 * G);
+        constexpr int64_t kSat = 512;
+        const int64_t ldu4 = ldu / 4;
+        auto pieces = [&](const void *kern, int G, auto launch) {
+            const int64_t waves = (P4 + 64 * G - 1) / (64 * G);
             const int64_t slots = (int64_t)resident_blocks(kern, kPipeBlock, 0) * (kPipeBlock / 64);
-            if (waves < slots) return -1.0;
-            return (double)waves / (double)(((waves + slots - 1) / slots) * slots);
+            const int64_t np = (waves + slots - 1) / slots;
+            const int64_t per = (waves + np - 1) / np;  // waves per piece, <= slots
+            if (per < kSat && G > 1) return false;
+            for (int64_t w0 = 0; w0 < waves; w0 += per) {
+                const int64_t c0 = w0 * 64 * G, c1 = min((w0 + per) * 64 * G, P4);  // f32x4 units
+                launch(dim3((unsigned)((min(per, waves - w0) + 3) / 4)), c0, c1 - c0);
+            }
+            return true;
         };
-        int64_t w22 = 0, w16 = 0;
-        const double e22 = fill(reinterpret_cast<const void *>(k_fedavg_exact_pipe<1, true, 22>), 22, w22);
-        const double e16 = fill(reinterpret_cast<const void *>(k_fedavg_exact_pipe<1, true, 16>), 16, w16);
-        if (e22 > 0 && e22 >= e16)
-            hipLaunchKernelGGL((k_fedavg_exact_pipe<1, true, 22>), dim3((unsigned)((w22 + 3) / 4)),
-                               dim3(kPipeBlock), 0, st, Uv, ldu / 4, rows, weight, (int)K, d, P4, ov);
-        else if (e16 > 0)
-            hipLaunchKernelGGL((k_fedavg_exact_pipe<1, true, 16>), dim3((unsigned)((w16 + 3) / 4)),
-                               dim3(kPipeBlock), 0, st, Uv, ldu / 4, rows, weight, (int)K, d, P4, ov);
-        else
-            hipLaunchKernelGGL((k_fedavg_exact_pipe<4, true, 1>),
-                               dim3((unsigned)((P4 + kPipeBlock - 1) / kPipeBlock)),
-                               dim3(kPipeBlock), 0, st, Uv, ldu / 4, rows, weight, (int)K, d, P4,
-                               ov);
+#define DLS_PIPE_PIECES(U_, G_)                                                              \
+    pieces(reinterpret_cast<const void *>(k_fedavg_exact_pipe<U_, true, G_>), G_,            \
+           [&](dim3 grid, int64_t c0, int64_t n4) {                                          \
+               hipLaunchKernelGGL((k_fedavg_exact_pipe<U_, true, G_>), grid, dim3(kPipeBlock), \
+                                  0, st, Uv + c0, ldu4, rows, weight, (int)K, d, n4, ov + c0); \
+           })
+        if (!DLS_PIPE_PIECES(1, 22) && !DLS_PIPE_PIECES(1, 16)) DLS_PIPE_PIECES(4, 1);
+#undef DLS_PIPE_PIECES
     } else if (mode == DLS_FEDAVG_FMA) {
         hipLaunchKernelGGL((k_fedavg_fma<8, true>), grid, dim3(kBlock), 0, st,
                            reinterpret_cast<const f32x4 *>(U), ldu / 4, rows, weight, (int)K, total,

@@ -51,7 +51,8 @@ def test_fedavg_golden_bit_exact():
 
 @pytest.mark.parametrize("K,P", [(1, 8), (3, 1028), (9, 4096 * 3 + 12), (64, 1036), (65, 2052),
                                  (100, 1 << 18), (131, 4100), (257, 1028),
-                                 (3, (1 << 22) + 1036), (65, (1 << 22) + 64 * 1024 + 12)])
+                                 (3, (1 << 22) + 1036), (65, (1 << 22) + 64 * 1024 + 12),
+                                 (7, 2_400_004), (5, 2_000_000)])
 def test_fedavg_random_bit_exact(K, P):
     g = torch.Generator().manual_seed(K * 7 + P)
     U = (torch.randn(K, P, generator=g) * 0.05).numpy()
