@@ -470,7 +470,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--clients", type=int, default=100, help="client updates per GPU")
-    ap.add_argument("--chunks", type=int, default=4, help="all-reduce pipeline chunks (N>1)")
+    ap.add_argument("--chunks", type=int, default=3, help="all-reduce pipeline chunks (N>1)")
     ap.add_argument("--subsets", type=int, default=50)
     ap.add_argument("--evals", type=int, default=8, help="timed Shapley utility evaluations")
     ap.add_argument("--eval-images", type=int, default=10000)

@@ -65,7 +65,7 @@ def chunk_bounds(P, chunks):
     return bounds
 
 
-def allreduce_chunked(flat, chunks=4, group=None, produce=None):
+def allreduce_chunked(flat, chunks=3, group=None, produce=None):
     """SUM all-reduce of a flat fp32 vector in ``chunks`` pieces (chunk_bounds).
 
     ``produce(c0, c1)`` (optional) fills flat[c0:c1] first; chunk c's all-reduce
@@ -105,7 +105,7 @@ class _ShardedMixin:
 class ShardedFedServer(_ShardedMixin, FedServer):
     """FedServer whose round is spread over all ranks (one process per GPU)."""
 
-    def __init__(self, group=None, chunks=4, **kwargs):
+    def __init__(self, group=None, chunks=3, **kwargs):
         self._init_shard(kwargs["worker_number"], group, chunks)
         super().__init__(**kwargs)
 
@@ -132,7 +132,7 @@ class ShardedFedServer(_ShardedMixin, FedServer):
 
 
 class ShardedFedQuantServer(_ShardedMixin, FedQuantServer):
-    def __init__(self, group=None, chunks=4, **kwargs):
+    def __init__(self, group=None, chunks=3, **kwargs):
         self._init_shard(kwargs["worker_number"], group, chunks)
         super().__init__(**kwargs)
 
