@@ -48,6 +48,7 @@ SIGNATURES = {
     "dls_last_error": ([], ctypes.c_char_p),
     "dls_abi_version": ([], _i32),
     "dls_device_count": ([], _i32),
+    "dls_two_constant_division": ([_f32], _i32),
     "dls_fedavg_f32": ([_p, _i64, _p, _p, _i32, _f32, _i64, _i32, _p, _p], _i32),
     "dls_subset_fedavg_f32": ([_p, _i64, _p, _p, _p, _p, _i32, _i64, _p, _i64, _p], _i32),
     "dls_subset_gemm_f32": ([_p, _i32, _i32, _p, _i64, _p, _i64, _p, _i64, _p], _i32),

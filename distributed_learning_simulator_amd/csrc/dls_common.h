@@ -54,10 +54,19 @@ inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 
 // building).  The kernels take the fast path for 2^-60 <= |a| <= 2^60 and
 // 1 <= b <= 2^31 (host side: `fast`) and fall back to IEEE `/` otherwise
 // (zeros incl. -0, denormals, inf, nan, huge values).
+//
+// Two-constant variant (Brisebarre, Muller & Raina, IEEE TC 2004): with
+// yh = RN(1/b), yl = RN(1/b - yh),  q = fma(a, yh, RN(a*yl))  is RN(a/b) for
+// every a for MOST divisors b (2 ops instead of 3).  Whether it holds for one b
+// is decided on the host by the same exhaustive mantissa check
+// (`two_constant_exact`, cached per b); `two` is set only when it passed and
+// a*yl stays normal over the fast range.
 struct FastDiv {
     float b;
     float y;
     int fast;
+    float yl;
+    int two;
 };
 
 inline FastDiv make_fastdiv(float b) {
@@ -65,7 +74,27 @@ inline FastDiv make_fastdiv(float b) {
     d.b = b;
     d.y = (float)(1.0 / (double)b);  // RN(1/b): double rounding is innocuous for '/'
     d.fast = (b >= 1.0f && b <= 2147483648.0f) ? 1 : 0;
+    d.yl = 0.f;
+    d.two = 0;
     return d;
+}
+
+// Exhaustive check of the two-constant division for divisor b (every fp32
+// mantissa of a in [1,2)); thread-safe, memoised per b (~ms on first use).
+bool two_constant_exact(float b, float yh, float yl);
+
+inline FastDiv make_fastdiv2(float b) {
+    FastDiv d = make_fastdiv(b);
+    if (!d.fast) return d;
+    d.yl = (float)(1.0 / (double)b - (double)d.y);
+    // fast-range a >= 2^-60: a*yl normal needs |yl| >= 2^-66 (yl == 0: b = 2^k)
+    const bool normal = d.yl == 0.f || (d.yl >= 0x1p-66f || d.yl <= -0x1p-66f);
+    d.two = (normal && two_constant_exact(b, d.y, d.yl)) ? 1 : 0;
+    return d;
+}
+
+__device__ __forceinline__ float div_two(float a, const FastDiv &d) {
+    return __builtin_fmaf(a, d.y, a * d.yl);
 }
 
 __device__ __forceinline__ float markstein(float a, float b, float y) {

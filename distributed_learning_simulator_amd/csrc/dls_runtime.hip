@@ -3,6 +3,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -75,9 +76,44 @@ hipStream_t side_stream() {
     return s;
 }
 
+// One block of mantissas; `target` lets the compiler vectorise the fma / div
+// (the box's and this container's hosts are AVX-512 EPYC / Xeon parts).
+__attribute__((target("avx2,fma"))) static bool two_constant_block(uint32_t m0, uint32_t n, float b,
+                                                                  float yh, float yl) {
+    int bad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t u = 0x3f800000u | (m0 + i);
+        float a;
+        memcpy(&a, &u, 4);
+        const float q = __builtin_fmaf(a, yh, a * yl);
+        bad |= (q != a / b);
+    }
+    return bad == 0;
+}
+
+bool two_constant_exact(float b, float yh, float yl) {
+    static std::mutex mu;
+    static std::unordered_map<uint32_t, bool> cache;
+    uint32_t key;
+    memcpy(&key, &b, 4);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    bool ok = true;
+    for (uint32_t m0 = 0; ok && m0 < (1u << 23); m0 += 4096) ok = two_constant_block(m0, 4096, b, yh, yl);
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = ok;
+    return ok;
+}
+
 }  // namespace dls
 
 extern "C" {
+
+int dls_two_constant_division(float divisor) { return dls::make_fastdiv2(divisor).two; }
+
 
 const char *dls_last_error(void) { return dls::g_last_error.c_str(); }
 

@@ -128,12 +128,15 @@ __device__ __forceinline__ float byte_val(uint32_t w, int k) {
     return (float)((w >> (8 * k)) & 0xffu);
 }
 
-template <bool ZFMA, bool FAST, bool SEXT = false>
+// TWO: the two-constant division q = fma(t, yh, RN(t*yl)) (dls_common.h), valid
+// for this divisor when the host's exhaustive check passed (d.two): 2 packed ops
+// per element pair instead of Markstein's 3.
+template <bool ZFMA, bool FAST, bool SEXT = false, bool TWO = false>
 __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s, float zs, float z,
                                             float wk, const FastDiv &d) {
     const f32x2 s2 = f32x2{s, s}, w2 = f32x2{wk, wk};
     const f32x2 nzs = f32x2{-zs, -zs}, z2 = f32x2{z, z};
-    const f32x2 b2 = f32x2{d.b, d.b}, y2 = f32x2{d.y, d.y};
+    const f32x2 b2 = f32x2{d.b, d.b}, y2 = f32x2{d.y, d.y}, yl2 = f32x2{d.yl, d.yl};
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
         const f32x2 x = f32x2{byte_val<SEXT>(qv[j >> 2], j & 3),
@@ -141,7 +144,9 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
         const f32x2 deq = ZFMA ? pk_fma(x, s2, nzs) : (x - z2) * s2;
         const f32x2 t = deq * w2;
         f32x2 q;
-        if (FAST) {
+        if (FAST && TWO) {
+            q = pk_fma(t, y2, t * yl2);
+        } else if (FAST) {
             const f32x2 q0 = t * y2;
             q = pk_fma(pk_fma(-q0, b2, t), y2, q0);
         } else {
@@ -164,7 +169,7 @@ struct QBatch {
     float s[U], z[U], wk[U];
 };
 
-template <bool SIGNED, int G>
+template <bool SIGNED, int G, bool TWO>
 __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8_t *__restrict__ Q,
                                                 const uint32_t (&qoff)[G], int64_t ldq,
                                                 const f32x2 *__restrict__ szc, SzLayout L,
@@ -213,7 +218,7 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8
                 if constexpr (COMMON) {
 #pragma unroll
                     for (int g = 0; g < GN; ++g)
-                        accum16_one<true, true, SIGNED>(acc[G0 + g], qv[g], sc, -zz, 0.f, wk, d);
+                        accum16_one<true, true, SIGNED, TWO>(acc[G0 + g], qv[g], sc, -zz, 0.f, wk, d);
                 } else {
                     const float zs = zz * sc;
                     const bool zfma = __builtin_fmaf(zz, sc, -zs) == 0.f;  // fl(z*s) exact
@@ -455,7 +460,7 @@ __device__ __forceinline__ void store16(const WaveTile &wt, float (&acc)[16],
 // One-channel tiles of up to 4 KiB: slice g of the tile is lanes'
 // 16-element chunks 1024 g + 16 lane; the wave walks the clients once for all
 // its slices (per-client table reads and readlanes amortised over G KiB).
-template <bool SIGNED, int G>
+template <bool SIGNED, int G, bool TWO>
 __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                           int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                           const int32_t *__restrict__ rows,
@@ -471,7 +476,7 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
         // idle lanes load a valid duplicate (loads stay unconditional)
         qoff[g] = (uint32_t)(wt.t.src + (e0 < wt.lenpad ? e0 : wt.lenpad - 16));  // ldq < 4 GiB
     }
-    int_one_channel<SIGNED, G>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
+    int_one_channel<SIGNED, G, TWO>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
     // transpose through LDS so that each store instruction writes 1 KiB contiguous
     __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
     float *mine = xs[threadIdx.x >> 6];
@@ -499,18 +504,19 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
 #ifndef DLS_QUANT_MINB
 #define DLS_QUANT_MINB 1
 #endif
-template <int G>
+template <int G, bool TWO>
 __global__ __launch_bounds__(kBlock, DLS_QUANT_MINB) void k_dequant_fast(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
     const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
-    // one launch per slice count G: each instance has its own register budget
+    // one launch per (slice count G, division method): each instance has its own
+    // register budget
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
     if (wt.t.kind == 1)
-        fast_tile<true, G>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        fast_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
     else
-        fast_tile<false, G>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        fast_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
@@ -751,7 +757,10 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     DLS_REQUIRE(ldq < ((int64_t)1 << 32), DLS_ELAYOUT,
                 "dls_dequant_fedavg: ldq=%lld must be < 2^32 (32-bit lane offsets)",
                 (long long)ldq);
-    const FastDiv d = make_fastdiv(total);
+#ifndef DLS_QUANT_TWO
+#define DLS_QUANT_TWO 1  // two-constant division when proven exact for N (0: always Markstein)
+#endif
+    const FastDiv d = DLS_QUANT_TWO ? make_fastdiv2(total) : make_fastdiv(total);
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
@@ -782,15 +791,15 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
         const int n = nfast[g];
         if (n == 0) return;
         const dim3 grid((unsigned)((n + wpb - 1) / wpb));
-#define DLS_FAST_LAUNCH(G_)                                                                       \
-    hipLaunchKernelGGL(k_dequant_fast<G_>, grid, dim3(kBlock), 0, s, tg[g], n,                    \
-                       reinterpret_cast<const uint8_t *>(Q), ldq, reinterpret_cast<const f32x2 *>(sz), \
-                       L, rows, weight, (int)K, d, out)
-        if (g == 0) DLS_FAST_LAUNCH(4);
-        else if (g == 1) DLS_FAST_LAUNCH(3);
-        else if (g == 2) DLS_FAST_LAUNCH(2);
-        else DLS_FAST_LAUNCH(1);
-#undef DLS_FAST_LAUNCH
+        using Kfn = void (*)(const dls_qtile *, int, const uint8_t *, int64_t, const f32x2 *,
+                             SzLayout, const int32_t *, const float *, int, FastDiv, float *);
+        static const Kfn kfast[4][2] = {{k_dequant_fast<4, false>, k_dequant_fast<4, true>},
+                                        {k_dequant_fast<3, false>, k_dequant_fast<3, true>},
+                                        {k_dequant_fast<2, false>, k_dequant_fast<2, true>},
+                                        {k_dequant_fast<1, false>, k_dequant_fast<1, true>}};
+        hipLaunchKernelGGL(kfast[g][d.two ? 1 : 0], grid, dim3(kBlock), 0, s, tg[g], n,
+                           reinterpret_cast<const uint8_t *>(Q), ldq,
+                           reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
     };
     if (DLS_QUANT_FORK == 2 && big >= 0) launch_fast(big, st);
     for (int g = 0; g < 4; ++g)

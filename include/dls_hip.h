@@ -56,6 +56,11 @@ typedef void *dls_stream_t;
 const char *dls_last_error(void);
 int dls_abi_version(void);
 int dls_device_count(void);
+/* 1 if the dequant kernels divide by `divisor` (= fl32(N), fed_server.py:60)
+ * with the two-constant method q = fma(a, yh, RN(a*yl)) — proven correctly
+ * rounded for this divisor by an exhaustive host-side mantissa check, cached —
+ * and 0 if they use the 3-op Markstein correction.  Host only; no GPU needed. */
+int dls_two_constant_division(float divisor);
 
 /* ------------------------------------------------------------------ FedAvg
  * Replaces FedServer.get_subset_model (servers/fed_server.py:44-66) for a

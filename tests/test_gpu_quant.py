@@ -212,3 +212,39 @@ def test_dequant_fedavg_chunked_clients_one_channel(K, L):
                 for k, v in p.items()} for p in payloads]
     ref = oquant.dequant_fedavg(clients, n, order, layout)
     assert same_bits(flat(out, layout), ref)
+
+
+@pytest.mark.parametrize("total,two", [(11735695, 0), (55123, 1), (1 << 20, 1)])
+def test_dequant_fedavg_division_methods(total, two):
+    """The bulk kernels divide by fl32(N) with the two-constant method when the
+    host's exhaustive check proves it exact for N, else with Markstein's
+    correction: both bit-exact vs the oracle (N = 11,735,695 fails the check,
+    55,123 passes it, 2^20 has yl = 0)."""
+    import ctypes
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
+    assert _native.lib().dls_two_constant_division(ctypes.c_float(total)) == two
+    g = torch.Generator().manual_seed(total)
+    C, L, K = 4, 4096, 3
+    n = [total // 3, total // 3, total - 2 * (total // 3)]
+    payloads = []
+    for k in range(K):
+        payloads.append({
+            "a": (torch.randint(-128, 128, (C, L), generator=g, dtype=torch.int8),
+                  torch.rand(C, generator=g, dtype=torch.float64) * 1e-2 + 1e-4,
+                  torch.zeros(C, dtype=torch.int64)),
+            "bias": torch.randn(C, generator=g),
+        })
+    store = QuantizedClientStore(payloads[0], dev, capacity=K)
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    assert store.nfast[0] == C
+    out = store.layout.views(store.fedavg(rows, n))
+    layout = [("a", (C, L)), ("bias", (C,))]
+    clients = [{k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy())
+                for k, v in p.items()} for p in payloads]
+    ref = oquant.dequant_fedavg(clients, n, list(range(K)), layout)
+    assert same_bits(flat(out, layout), ref)

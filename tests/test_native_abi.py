@@ -58,3 +58,25 @@ def test_product_path_has_no_oracle_import():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle\b", src, re.M), f
+
+
+def test_two_constant_division_check_without_gpu(lib):
+    """dls_two_constant_division's host-side exhaustive check agrees with an
+    independent numpy restatement of fma(a, yh, RN(a*yl)) == RN(a/b) over every
+    fp32 mantissa (float64 products are exact for the fma's 48-bit product)."""
+    import numpy as np
+    f = lib.dls_two_constant_division
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_float]
+    a = (np.arange(1 << 23, dtype=np.uint32) | np.uint32(0x3F800000)).view(np.float32)
+    for b in (55123.0, 49972.0, 1024.0, 3.0, 7.0, 100.0):
+        b32 = np.float32(b)
+        yh = np.float32(1.0 / float(b32))
+        yl = np.float32(1.0 / float(b32) - float(yh))
+        lo = (a * yl).astype(np.float32)  # RN(a*yl)
+        # fma: exact a*yh + lo in float64 (a*yh has <= 48 significant bits; the
+        # sum is exact unless exponents differ wildly, which they do not here),
+        # then one rounding to fp32
+        q = (a.astype(np.float64) * np.float64(yh) + np.float64(lo)).astype(np.float32)
+        expect = int(np.array_equal(q, a / b32))
+        assert f(b) == expect, b
+    assert f(0.5) == 0  # outside the fast range: never two-constant
