@@ -56,7 +56,10 @@ __device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *
 
 // grid: x = blocks of 4 waves x kPackTPW tiles, y = client.  Each wave issues
 // the loads of its kPackTPW tiles before packing any (memory-level parallelism).
-constexpr int kPackTPW = 4;
+#ifndef DLS_PACK_TPW
+#define DLS_PACK_TPW 4
+#endif
+constexpr int kPackTPW = DLS_PACK_TPW;
 
 __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ X, int64_t ldx,
                                                       int64_t P, uint64_t *__restrict__ planes,
@@ -140,6 +143,12 @@ struct HSCounter {
 // the wave writes its 4096 outputs coalesced, a 16-lane group per 64-parameter
 // group, instead of 64 lanes each scattering 256 bytes.
 constexpr int kVoteBlock = 64;
+#ifndef DLS_VOTE_G
+#define DLS_VOTE_G 4  // groups per lane on large models (each wave streams G KB per client)
+#endif
+#ifndef DLS_VOTE_DBG
+#define DLS_VOTE_DBG 1  // widest G whose 8-client batches are double-buffered
+#endif
 
 
 template <int CB, bool ROWS, int G>
@@ -181,7 +190,7 @@ __device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes,
     // batches of 8 clients, double-buffered; loads inside the steady-state loop
     // are unconditional so every consume waits with an exact vmcnt
     const int nb = K / B8;
-    if (G > 1) {  // one batch (8 clients x G KB) in flight per wave: register budget
+    if (G > DLS_VOTE_DBG) {  // one batch (8 clients x G KB) in flight per wave: register budget
         for (int b = 0; b < nb; ++b) {
             u64x2 wa[G][B8];
             load8(b * B8, wa);
@@ -455,14 +464,15 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
     // 4 groups per lane (each wave streams 4 KB of every client row, measured
     // 12 % faster than 1 KB at P = 11.2M) while that still leaves >= 2 waves per
     // CU; 1 group per lane (double-buffered batches) for small models
-    const bool wide = CB <= 12 && (vote_groups + 255) / 256 >= 512;
-    const dim3 grid((unsigned)(wide ? (vote_groups + 255) / 256 : (vote_groups + 63) / 64));
+    constexpr int GW = DLS_VOTE_G;
+    const bool wide = CB <= 12 && (vote_groups + 64 * GW - 1) / (64 * GW) >= 512;
+    const dim3 grid((unsigned)(wide ? (vote_groups + 64 * GW - 1) / (64 * GW) : (vote_groups + 63) / 64));
 #define DLS_VOTE_LAUNCH(C_, G_)                                                              \
     hipLaunchKernelGGL((k_sign_vote<CB, C_, G_>), grid, dim3(kVoteBlock), 0, st, planes, ldp, \
                        rows, K, P, ngroups, counts, sign_out, vote_planes, vote_groups)
-    if (counts && wide) DLS_VOTE_LAUNCH(true, 4);
+    if (counts && wide) DLS_VOTE_LAUNCH(true, GW);
     else if (counts) DLS_VOTE_LAUNCH(true, 1);
-    else if (wide) DLS_VOTE_LAUNCH(false, 4);
+    else if (wide) DLS_VOTE_LAUNCH(false, GW);
     else DLS_VOTE_LAUNCH(false, 1);
 #undef DLS_VOTE_LAUNCH
     return check_launch("dls_sign_vote");
