@@ -38,6 +38,20 @@ def values(path, counter, kernel):
     return out
 
 
+# C-ABI calls a workload's bench.py function makes for its --steps / --warmup
+# (bench.bench_fedavg: warmup + steps; bench.bench_fedavg_k1000: 2 + max(3, steps // 4))
+CALLS = {"headline": lambda s, w: s + w, "fedavg_k1000": lambda s, w: 2 + max(3, s // 4)}
+
+
+def bench_calls(path, wl):
+    """C-ABI calls the PMC pass of workload wl made (from its bench.py line), or None."""
+    try:
+        d = json.loads(open(path).read().strip().splitlines()[-1])
+        return CALLS[wl](int(d["steps"]), int(d["warmup"]))
+    except (OSError, ValueError, KeyError, IndexError):
+        return None
+
+
 def main(tag):
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     res, lines = {}, []
@@ -52,11 +66,18 @@ def main(tag):
                                             "run_counter_collection.csv"), "FETCH_SIZE", name)
                     w = values(os.path.join(base, f"pmc_{wl}_WRITE_SIZE",
                                             "run_counter_collection.csv"), "WRITE_SIZE", name)
-                    # every instance (e.g. k_dequant_fast<4..1>) runs once per call
+                    calls = bench_calls(os.path.join(base, f"pmc_{wl}_FETCH_SIZE.json"), wl)
                     for inst in f.keys() & w.keys():
-                        fm += statistics.median(f[inst])
-                        wm += statistics.median(w[inst])
-                        nl = max(nl, len(f[inst]))
+                        if calls and len(f[inst]) % calls == 0 and len(w[inst]) % calls == 0:
+                            # one C-ABI call may launch an instance several times
+                            # (FedAvg's one-generation pieces): bytes per call
+                            fm += sum(f[inst]) / calls
+                            wm += sum(w[inst]) / calls
+                            nl = max(nl, calls)
+                        else:  # every instance (e.g. k_dequant_fast<4..1>) once per call
+                            fm += statistics.median(f[inst])
+                            wm += statistics.median(w[inst])
+                            nl = max(nl, len(f[inst]))
             except OSError:
                 continue
             if not nl:
@@ -67,7 +88,7 @@ def main(tag):
                         "hbm_bytes_per_launch": rd + wr, "launches": nl}
             lines.append(f"{key:14s} {kernel:36s} FETCH_SIZE {fm:12.0f} KiB (x2 -> {rd / 1e9:8.3f} GB) "
                          f"WRITE_SIZE {wm:11.0f} KiB ({wr / 1e9:7.3f} GB) total "
-                         f"{(rd + wr) / 1e9:8.3f} GB/launch  [{nl} launches]")
+                         f"{(rd + wr) / 1e9:8.3f} GB/call  [{nl} calls]")
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.txt"), "w") as fh:

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace --stats run: per-kernel calls / avg / min / max.
 
-    python tools/trace_summary.py gpurun_out/prof_r01/trace/run_kernel_stats.csv > profiles/r01_kernel_stats.txt
+    python tools/trace_summary.py gpurun_out/prof_r01/trace/run_kernel_stats.csv [CALLS] > profiles/r01_kernel_stats.txt
+
+With CALLS (the number of C-ABI calls the traced command made), also prints the
+kernel time per call: one dls_fedavg_f32 call may launch its kernel as several
+one-generation pieces, so rocprof's per-launch average is a fraction of the
+per-call duration bench.py times with HIP events.
 """
 import csv
 import re
@@ -13,7 +18,7 @@ def short(name):
     return m.group(1) if m else name[:60]
 
 
-def main(path):
+def main(path, calls=None):
     rows = list(csv.DictReader(open(path)))
     print(f"# rocprofv3 --kernel-trace --stats summary of {path}")
     print(f"{'kernel':44s} {'calls':>6s} {'avg_us':>10s} {'min_us':>10s} {'max_us':>10s} {'share%':>7s}")
@@ -23,7 +28,12 @@ def main(path):
         print(f"{short(r['Name']):44s} {int(r['Calls']):6d} {float(r['AverageNs']) / 1e3:10.2f} "
               f"{float(r['MinNs']) / 1e3:10.2f} {float(r['MaxNs']) / 1e3:10.2f} "
               f"{float(r['Percentage']):7.2f}")
+    if calls:
+        tot = sum(float(r["TotalDurationNs"]) for r in rows if "dls::" in r["Name"])
+        n = sum(int(r["Calls"]) for r in rows if "dls::" in r["Name"])
+        print(f"# per C-ABI call: {n} kernel launches / {calls} calls, "
+              f"{tot / calls / 1e3:.2f} us of kernel time per call")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
