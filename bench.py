@@ -37,7 +37,7 @@ sys.path.insert(0, ROOT)
 
 from distributed_learning_simulator_amd import _native  # noqa: E402
 from distributed_learning_simulator_amd.layout import ParameterLayout  # noqa: E402
-from distributed_learning_simulator_amd.distributed import chunk_bounds  # noqa: E402
+from distributed_learning_simulator_amd.distributed import allreduce_chunked, chunk_bounds  # noqa: E402
 from distributed_learning_simulator_amd.model_shapes import resnet18_cifar, vgg16  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -229,28 +229,107 @@ def bench_sign(args, dev):
     }
 
 
-def bench_quant(args, dev):
+def _quant_store(dev, K, seed):
+    """K synthetic VGG-16 int8 payloads (per-channel symmetric) in a device store."""
     from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
-    shapes = vgg16()
-    K = 100
     template = {}
-    for name, s in shapes:
+    for name, s in vgg16():
         if len(s) >= 2:
             template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
                               torch.zeros(s[0], dtype=torch.int64))
         else:
             template[name] = torch.zeros(s)
     store = QuantizedClientStore(template, dev, capacity=K)
-    g = torch.Generator(device=dev).manual_seed(SEED + 4)
+    g = torch.Generator(device=dev).manual_seed(seed)
     store.Q.random_(0, 256, generator=g)  # int8 payload bytes
     store.F.normal_(generator=g).mul_(0.01)
     store.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
     store.sz[..., 1].zero_()
-    rows = list(range(K))
     store._free = []
     n = torch.randint(100, 1001, (K,), generator=g, device=dev).tolist()
+    ql = store.qlayout
+    Pq = sum(m for m, k in zip(store.layout.numels, ql.kinds) if k)
+    Pf = sum(m for m, k in zip(store.layout.numels, ql.kinds) if not k)
+    return store, n, Pq + 4 * Pf + 8 * ql.C, Pq + Pf
+
+
+# ------------------------------------------------- sharded servers (N > 1)
+def _max_over_ranks(wall, dev):
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_sign_sharded(args, dev, world, rank):
+    """ShardedSignSGDServer's round (distributed.py): every rank votes its own 1000
+    clients into int32 counts, RCCL int32 SUM all-reduce, counts -> fp32 signs +
+    packed vote on every rank.  Weak scaling: 1000 clients per GPU."""
+    layout = ParameterLayout(resnet18_cifar())
+    P, K = layout.P, 1000
+    W = _native.sign_words(P)
+    g = torch.Generator(device=dev).manual_seed(SEED + 30 + rank)
+    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]
+    counts = torch.empty(P, dtype=torch.int32, device=dev)
+    sign_out = torch.empty(P, device=dev)
+    vote = torch.empty(W, dtype=torch.int64, device=dev)
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.sign_vote_count(planes, None, K, P, counts)
+        if b is not None:
+            b.record()
+        dist.all_reduce(counts)
+        _native.sign_from_counts(counts, P, sign_out, vote)
+
+    wall, kms = timed_launches(step, args.steps, args.warmup, dist.barrier)
+    ms = _max_over_ranks(wall, dev) / args.steps * 1e3
+    del planes
+    return {"config": f"signSGD majority vote sharded over {world} GPUs: 1000 clients x ResNet-18 "
+                      "per GPU, int32 counts + RCCL all-reduce + signs / packed vote on every rank",
+            "value": round(world * K * W * 8 / (ms / 1e3) / 1e9, 2),
+            "unit": "GB/s (packed client updates, all ranks)", "ms_per_step": round(ms, 4),
+            "count_kernel_us": round(sum(kms) / len(kms) * 1e3, 2)}
+
+
+def bench_quant_sharded(args, dev, world, rank):
+    """ShardedFedQuantServer's round: every rank dequant-averages its own 100 VGG-16
+    clients with the global sample count, then a chunked fp32 SUM all-reduce of
+    the 553 MB aggregate.  Weak scaling: 100 clients per GPU."""
+    store, n, client_bytes, _ = _quant_store(dev, 100, SEED + 40 + rank)
+    K = len(n)
+    n_all = torch.tensor([sum(n)], dtype=torch.float64, device=dev)
+    dist.all_reduce(n_all)
+    total = float(n_all.item())
     out = torch.empty(store.layout.P, device=dev)
-    rows_t = torch.tensor(rows, dtype=torch.int32, device=dev)
+    rows_t = torch.arange(K, dtype=torch.int32, device=dev)
+    w_t = torch.tensor(n, dtype=torch.float32, device=dev)
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.dequant_fedavg(store.tiles, store.ntiles, store.nfast, store.Q, store.F, store.sz,
+                               rows_t, w_t, total, out)
+        if b is not None:
+            b.record()
+        allreduce_chunked(out, args.chunks)
+
+    wall, kms = timed_launches(step, args.steps, args.warmup, dist.barrier)
+    ms = _max_over_ranks(wall, dev) / args.steps * 1e3
+    del store
+    return {"config": f"fed_quant 8-bit sharded over {world} GPUs: 100 VGG-16 clients per GPU, "
+                      "fused dequant + FedAvg, chunked RCCL fp32 all-reduce",
+            "value": round(world * K * client_bytes / (ms / 1e3) / 1e9, 2),
+            "unit": "GB/s (int8 client updates, all ranks)", "ms_per_step": round(ms, 4),
+            "dequant_kernel_us": round(sum(kms) / len(kms) * 1e3, 2)}
+
+
+def bench_quant(args, dev):
+    store, n, client_bytes, p_logical = _quant_store(dev, 100, SEED + 4)
+    K = len(n)
+    out = torch.empty(store.layout.P, device=dev)
+    rows_t = torch.arange(K, dtype=torch.int32, device=dev)
     w_t = torch.tensor(n, dtype=torch.float32, device=dev)
     total = float(sum(n))
 
@@ -264,17 +343,13 @@ def bench_quant(args, dev):
 
     wall, kms = timed_launches(step, args.steps, args.warmup)
     ms = wall / args.steps * 1e3
-    ql = store.qlayout
-    Pq = sum(m for m, k in zip(store.layout.numels, ql.kinds) if k)
-    Pf = sum(m for m, k in zip(store.layout.numels, ql.kinds) if not k)
-    client_bytes = Pq + 4 * Pf + 8 * ql.C
     bytes_per_launch = K * client_bytes + 4 * store.layout.numel
     del store
     return {
         "config": "fed_quant 8-bit, 100 clients x VGG-16, fused dequant + FedAvg (bit-exact)",
         "value": round(K * client_bytes / (ms / 1e3) / 1e9, 2),
         "unit": "GB/s (int8 client updates)",
-        "fp32_logical_GBps": round(K * (Pq + Pf) * 4 / (ms / 1e3) / 1e9, 2),
+        "fp32_logical_GBps": round(K * p_logical * 4 / (ms / 1e3) / 1e9, 2),
         "ms_per_step": round(ms, 4),
         "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms, key="fed_quant"),
     }
@@ -478,6 +553,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--only", default="", help="comma list: headline,fedavg_k1000,sign_vote,"
+                    "sign_vote_sharded,fed_quant_sharded,"
                                                 "fed_quant,shapley_gemm,shapley_evals")
     ap.add_argument("--cpu-clients", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -502,6 +578,15 @@ def main():
     if only is None or "headline" in only:
         value, ms, rf, extra = bench_fedavg(args, dev, rank, world)
     components = {}
+    if world > 1 and not args.quick:  # the sharded servers' rounds: every rank takes part
+        for name, fn in (("sign_vote_sharded", bench_sign_sharded),
+                         ("fed_quant_sharded", bench_quant_sharded)):
+            if only is not None and name not in only:
+                continue
+            components[name] = fn(args, dev, world, rank)  # collective: no per-rank skipping
+            if rank == 0:
+                log(name, json.dumps(components[name]))
+            torch.cuda.empty_cache()
     if not args.quick and rank == 0:
         for name, fn in (("fedavg_k1000", bench_fedavg_k1000), ("sign_vote", bench_sign),
                          ("fed_quant", bench_quant),
