@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("DLS_HIP_LIB", os.path.join(_HERE, "libdls_hip.so"))
 FEDAVG_EXACT = 0
 FEDAVG_FMA = 1
 SIGN_NAN_MARK = 1 << 24
+SUBSET_UNION_MAX = 64  # DLS_SUBSET_UNION_MAX: coalitions per dls_subset_fedavg_union_f32 call
 
 
 def sign_words(P):
@@ -51,6 +52,8 @@ SIGNATURES = {
     "dls_two_constant_division": ([_f32], _i32),
     "dls_fedavg_f32": ([_p, _i64, _p, _p, _i32, _f32, _i64, _i32, _p, _p], _i32),
     "dls_subset_fedavg_f32": ([_p, _i64, _p, _p, _p, _p, _i32, _i64, _p, _i64, _p], _i32),
+    "dls_subset_fedavg_union_f32": ([_p, _i64, _p, _p, _p, _i32, _p, _i32, _i64, _p, _i64, _p],
+                                    _i32),
     "dls_subset_gemm_f32": ([_p, _i32, _i32, _p, _i64, _p, _i64, _p, _i64, _p], _i32),
     "dls_sign_pack_f32": ([_p, _i64, _i32, _i64, _p, _i64, _p, _p], _i32),
     "dls_sign_vote_count": ([_p, _i64, _p, _i32, _i64, _p, _p], _i32),
@@ -135,6 +138,19 @@ def subset_fedavg(U, sub_off, sub_rows, sub_weight, sub_total, P, out, stream=No
     _check(lib().dls_subset_fedavg_f32(_ptr(U), U.stride(0), _ptr(sub_off), _ptr(sub_rows),
                                        _ptr(sub_weight), _ptr(sub_total), S, P, _ptr(out),
                                        out.stride(0), _stream(stream, U)), "dls_subset_fedavg_f32")
+    return out
+
+
+def subset_fedavg_union(U, urows, uweight, member, sub_total, P, out, stream=None):
+    """S <= SUBSET_UNION_MAX coalitions over one client union, each client row read
+    once (dls_subset_fedavg_union_f32); member: int64 [Ku] bit masks."""
+    assert urows.dtype == torch.int32 and uweight.dtype == torch.float32
+    assert member.dtype == torch.int64 and sub_total.dtype == torch.float32
+    S = sub_total.numel()
+    _check(lib().dls_subset_fedavg_union_f32(_ptr(U), U.stride(0), _ptr(urows), _ptr(uweight),
+                                             _ptr(member), urows.numel(), _ptr(sub_total), S, P,
+                                             _ptr(out), out.stride(0), _stream(stream, U)),
+           "dls_subset_fedavg_union_f32")
     return out
 
 

@@ -11,6 +11,7 @@ HBM layout:
   order — but the dict values are views of the client's row in ``U``, so the
   reference hooks and user code still see per-tensor dicts.
 """
+import heapq
 import threading
 
 import torch
@@ -25,6 +26,56 @@ def _i32(xs, device):
 
 def _f32(xs, device):
     return torch.tensor(list(xs), dtype=torch.float32).to(device, non_blocking=True)
+
+
+def union_order(subsets):
+    """One client order that lists every subset's clients in that subset's own
+    order (a topological merge of the subsets), or None if there is none (two
+    subsets order a pair of clients differently, or a subset repeats a client).
+    Ties go to the client seen first, so sorted subsets give the sorted union."""
+    first, succ, indeg = {}, {}, {}
+    for sub in subsets:
+        if len(set(sub)) != len(sub):
+            return None
+        for c in sub:
+            if c not in first:
+                first[c] = len(first)
+                succ[c] = set()
+                indeg[c] = 0
+        for a, b in zip(sub, sub[1:]):
+            if b not in succ[a]:
+                succ[a].add(b)
+                indeg[b] += 1
+    ready = [(first[c], c) for c in first if indeg[c] == 0]
+    heapq.heapify(ready)
+    order = []
+    while ready:
+        _, c = heapq.heappop(ready)
+        order.append(c)
+        for b in succ[c]:
+            indeg[b] -= 1
+            if indeg[b] == 0:
+                heapq.heappush(ready, (first[b], b))
+    return order if len(order) == len(first) else None
+
+
+def union_batch(subsets, n_of_row, device):
+    """Device tables of dls_subset_fedavg_union_f32 for <= 64 subsets (row lists)
+    over one union order: (urows int32, uweight fp32, member int64 masks,
+    sub_total fp32), or None when no common order exists."""
+    order = union_order(subsets)
+    if order is None:
+        return None
+    pos = {r: j for j, r in enumerate(order)}
+    member = [0] * len(order)
+    for s, sub in enumerate(subsets):
+        for r in sub:
+            member[pos[r]] |= 1 << s
+    member = [m - (1 << 64) if m >= 1 << 63 else m for m in member]  # as int64
+    totals = [float(sum(int(n_of_row[r]) for r in sub)) for sub in subsets]
+    return (_i32(order, device), _f32([int(n_of_row[r]) for r in order], device),
+            torch.tensor(member, dtype=torch.int64).to(device, non_blocking=True),
+            _f32(totals, device))
 
 
 class ClientUpdateStore:
@@ -91,6 +142,17 @@ class ClientUpdateStore:
         P = self.layout.P
         if out is None:
             out = torch.empty((S, P), dtype=torch.float32, device=self.device)
+        if method == "exact" and all(subsets):
+            # each client row read once per batch of <= 64 coalitions (the union
+            # kernel), when one client order suits every coalition (always for the
+            # Shapley servers' sorted tuples); else one coalition per grid row
+            tables = [union_batch(subsets[c0:c0 + _native.SUBSET_UNION_MAX], n_of_row, self.device)
+                      for c0 in range(0, S, _native.SUBSET_UNION_MAX)]
+            if all(t is not None for t in tables):
+                for i, t in enumerate(tables):
+                    c0 = i * _native.SUBSET_UNION_MAX
+                    _native.subset_fedavg_union(self.U, *t, P, out[c0:c0 + t[3].numel()])
+                return out
         if method == "exact":
             off, flat_rows, flat_w, totals = [0], [], [], []
             for sub in subsets:

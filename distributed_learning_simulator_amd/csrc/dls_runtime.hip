@@ -59,19 +59,26 @@ int resident_blocks(const void *kernel, int block, size_t lds) {
     return n;
 }
 
-hipStream_t side_stream() {
+hipStream_t side_stream(hipStream_t parent) {
     // one non-blocking stream per device, created on first use and kept for the
     // process (the library's launchers fork small concurrent kernels onto it and
-    // join back to the caller's stream before returning)
+    // join back to the caller's stream before returning).  The device is the
+    // parent stream's, not the calling thread's current device: worker threads
+    // may launch on tensors of another GPU than the one they have selected.
     static std::mutex mu;
     static std::unordered_map<int, hipStream_t> streams;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (hipStreamGetDevice(parent, &dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(mu);
     auto it = streams.find(dev);
     if (it != streams.end()) return it->second;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e != hipSuccess) return nullptr;
     streams[dev] = s;
     return s;
 }

@@ -209,6 +209,169 @@ __global__ __launch_bounds__(kBlock) void k_subset_exact(const f32x4 *__restrict
     out[(int64_t)s * ldo4 + i] = acc;
 }
 
+// Batched reference-order subsets over a client "union" (the Shapley servers'
+// default path, servers/GTG_shapley_value_server.py:56 and
+// servers/multiround_shapley_value_server.py:37).  The batch's S coalitions are
+// all made of the union's Ku clients, and walking the union in its order visits
+// every coalition's members in that coalition's own order (the host orders the
+// union so; sorted worker-id tuples always are).  So each client row is read
+// from HBM once per batch instead of once per coalition containing it:
+//   for client j of the union:  t = fl(x * fl32(n_j))
+//       for every coalition s holding j (bit s of member[j]):  acc_s = fl(acc_s + fl(t / N_s))
+// which is term for term the op sequence of servers/fed_server.py:57-65 for
+// each coalition (acc_s starts at -0: -0 + q == q, "the first client is assigned").
+//
+// Block = one tile of 256 parameters (a lane owns 4), one wave per <= kSubsetSB
+// coalitions (spread evenly): the waves of a block load the same 1 KiB of each client row at the
+// same time (one HBM read, the others served by the CU's L1 / the XCD's L2) and
+// each keeps its kSubsetSB accumulators in registers.  Membership is a
+// wave-uniform bit test (SALU branch), so a coalition that does not hold client
+// j costs nothing.  Algorithmic bytes: (Ku + S) * 4 per parameter; VALU: 4 per
+// parameter per (client, coalition) membership (multiply-add Markstein division +
+// add) + 4 per parameter per (client, wave) for t.  At S = Ku = 50 with
+// coalitions half full the VALU issue, not HBM, is the roof.
+#ifndef DLS_SUBSET_SB
+#define DLS_SUBSET_SB 8  // coalitions per wave: 10 VGPRs each (SB 8 -> 135 VGPRs, 3 waves / SIMD)
+#endif
+#ifndef DLS_SUBSET_UB
+#define DLS_SUBSET_UB 4  // clients per double-buffered batch
+#endif
+constexpr int kSubsetSB = DLS_SUBSET_SB;
+constexpr int kSubsetUB = DLS_SUBSET_UB;
+constexpr int kSubsetMaxBlock = 64 * ((DLS_SUBSET_UNION_MAX + kSubsetSB - 1) / kSubsetSB);
+
+template <int SB, int UB>
+__global__ __launch_bounds__(kSubsetMaxBlock) void k_subset_union(const f32x4 *__restrict__ Uv, int64_t ldu4,
+                                                      const int32_t *__restrict__ urows,
+                                                      const float *__restrict__ uw,
+                                                      const uint64_t *__restrict__ member, int Ku,
+                                                      const float *__restrict__ sub_total, int S,
+                                                      int64_t P4, f32x4 *__restrict__ out,
+                                                      int64_t ldo4) {
+    const int lane = __lane_id();
+    // the S coalitions are spread evenly over the block's waves (<= SB each)
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nwv = blockDim.x >> 6;
+    const int s0 = wv * S / nwv;
+    const int ns = (wv + 1) * S / nwv - s0;  // wave-uniform, 1..SB by the launch geometry
+    const int64_t i0 = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t iq = i0 < P4 ? i0 : P4 - 1;  // every lane stays: the tables need all 64
+    // per-coalition divisor N_s and y_s = RN(1/N_s) (wave-uniform values, kept in
+    // VGPRs: 2*SB SGPRs beside the client tables would spill)
+    float bs[SB];
+    f32x2 ys[SB];  // {y, y}: the packed multiply-adds take it as a register pair
+    int allfast = 1;
+#pragma unroll
+    for (int s = 0; s < SB; ++s) {
+        bs[s] = s < ns ? sub_total[s0 + s] : 1.f;
+        const float y = (float)(1.0 / (double)bs[s]);
+        ys[s] = f32x2{y, y};
+        allfast &= (int)(bs[s] >= 1.0f && bs[s] <= 2147483648.0f);
+    }
+    f32x4 acc[SB];
+#pragma unroll
+    for (int s = 0; s < SB; ++s) acc[s] = f32x4{-0.f, -0.f, -0.f, -0.f};
+    const uint32_t smask = (uint32_t)((1ull << ns) - 1ull);
+    // client table: lane l holds client (chunk base + l); the next chunk is in flight
+    auto fetch = [&](int k, int &r, float &w, uint32_t &m) {
+        const int kk = min(k + lane, Ku - 1);
+        r = urows[kk];
+        w = uw[kk];
+        m = k + lane < Ku ? (uint32_t)(member[kk] >> s0) & smask : 0u;  // past the end: no work
+    };
+    int nr;
+    float nw;
+    uint32_t nm;
+    fetch(0, nr, nw, nm);
+    // Common case only: every t of the wave in Markstein's range and every
+    // divisor in [1, 2^31].  Otherwise (zeros, denormals, huge values, inf / nan)
+    // the wave flags `redo` and recomputes its tile after the loop on a slow,
+    // compact path, so the hot loop carries no fix-up code or registers.
+    int redo = !allfast;
+    auto one = [&](f32x4 x, float wk, uint32_t m) {
+        f32x4 t;
+        t.x = x.x * wk;
+        t.y = x.y * wk;
+        t.z = x.z * wk;
+        t.w = x.w * wk;
+        const int ok = (int)in_fast_range(t.x) & (int)in_fast_range(t.y) &
+                       (int)in_fast_range(t.z) & (int)in_fast_range(t.w);
+        redo |= (int)(__ballot(!ok) != 0);
+#pragma unroll
+        for (int s = 0; s < SB; ++s) {
+            if (m & (1u << s)) {  // wave-uniform: a scalar branch
+                // Markstein on element pairs (v_pk_mul / v_pk_fma: the scalar ops' roundings)
+                const f32x2 b2 = f32x2{bs[s], bs[s]};
+                const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
+                const f32x2 ql0 = tl * ys[s], qh0 = th * ys[s];
+                const f32x2 ql = __builtin_elementwise_fma(
+                    __builtin_elementwise_fma(-ql0, b2, tl), ys[s], ql0);
+                const f32x2 qh = __builtin_elementwise_fma(
+                    __builtin_elementwise_fma(-qh0, b2, th), ys[s], qh0);
+                acc[s] = add4(acc[s], f32x4{ql.x, ql.y, qh.x, qh.y});
+            }
+        }
+    };
+    for (int base = 0; base < Ku; base += 64) {
+        const int tr = nr;
+        const float tw = nw;
+        const uint32_t tm = nm;
+        fetch(base + 64, nr, nw, nm);
+        // batches of UB clients, double-buffered; past the chunk's end a batch
+        // loads a valid duplicate row with no membership (no work), so every load
+        // is unconditional (exact vmcnt waits) and there is no tail loop
+        const int nb = (min(64, Ku - base) + UB - 1) / UB;
+        auto load = [&](int j0, f32x4 (&x)[UB], float (&wk)[UB], uint32_t (&mk)[UB]) {
+#pragma unroll
+            for (int u = 0; u < UB; ++u) {
+                const int j = min(j0 + u, 63);
+                const int64_t r = __builtin_amdgcn_readlane(tr, j);
+                wk[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
+                mk[u] = j0 + u < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)tm, j) : 0u;
+                x[u] = load4<false>(Uv + r * ldu4 + iq);
+            }
+        };
+        f32x4 xA[UB], xB[UB];
+        float wA[UB], wB[UB];
+        uint32_t mA[UB], mB[UB];
+        load(0, xA, wA, mA);
+        for (int b = 0; b < nb; b += 2) {
+            load((b + 1) * UB, xB, wB, mB);
+#pragma unroll
+            for (int u = 0; u < UB; ++u) one(xA[u], wA[u], mA[u]);
+            load((b + 2) * UB, xA, wA, mA);
+            if (b + 1 < nb) {
+#pragma unroll
+                for (int u = 0; u < UB; ++u) one(xB[u], wB[u], mB[u]);
+            }
+        }
+    }
+    if (__builtin_expect(!redo, 1)) {
+        if (i0 < P4) {
+#pragma unroll
+            for (int s = 0; s < SB; ++s)
+                if (s < ns) out[(int64_t)(s0 + s) * ldo4 + iq] = acc[s];
+        }
+        return;
+    }
+    // slow path (acc is dead here): one coalition at a time, guarded division
+    for (int s = 0; s < ns; ++s) {
+        FastDiv d;
+        d.b = sub_total[s0 + s];
+        d.y = (float)(1.0 / (double)d.b);
+        d.fast = d.b >= 1.0f && d.b <= 2147483648.0f;
+        f32x4 a = f32x4{-0.f, -0.f, -0.f, -0.f};
+        for (int j = 0; j < Ku; ++j) {
+            if (!((member[j] >> (s0 + s)) & 1u)) continue;
+            const f32x4 x = load4<false>(Uv + (int64_t)urows[j] * ldu4 + iq);
+            const float wk = uw[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[e] += div_exact(x[e] * wk, d);
+        }
+        if (i0 < P4) out[(int64_t)(s0 + s) * ldo4 + iq] = a;
+    }
+}
+
 }  // namespace
 }  // namespace dls
 
@@ -293,4 +456,29 @@ extern "C" int dls_subset_fedavg_f32(const float *U, int64_t ldu, const int32_t 
                        sub_rows, sub_weight, sub_total, (int)S, P4, reinterpret_cast<f32x4 *>(out),
                        ldo / 4);
     return check_launch("dls_subset_fedavg_f32");
+}
+
+extern "C" int dls_subset_fedavg_union_f32(const float *U, int64_t ldu, const int32_t *urows,
+                                           const float *uweight, const uint64_t *member, int32_t Ku,
+                                           const float *sub_total, int32_t S, int64_t P,
+                                           float *out, int64_t ldo, dls_stream_t stream) {
+    DLS_REQUIRE(U && urows && uweight && member && sub_total && out, DLS_EINVAL,
+                "dls_subset_fedavg_union_f32: null pointer");
+    DLS_REQUIRE(Ku > 0 && P > 0 && S > 0 && S <= DLS_SUBSET_UNION_MAX, DLS_EINVAL,
+                "dls_subset_fedavg_union_f32: Ku=%d S=%d (1..%d) P=%lld", Ku, S,
+                DLS_SUBSET_UNION_MAX, (long long)P);
+    DLS_REQUIRE(P % 4 == 0 && ldu % 4 == 0 && ldo % 4 == 0 && ldu >= P && ldo >= P, DLS_ELAYOUT,
+                "dls_subset_fedavg_union_f32: P, ldu, ldo must be multiples of 4");
+    DLS_REQUIRE(aligned16(U) && aligned16(out), DLS_ELAYOUT,
+                "dls_subset_fedavg_union_f32: 16-byte alignment");
+    static_assert(kSubsetMaxBlock <= 1024, "at most 16 waves per block");
+    const int64_t P4 = P / 4;
+    const int64_t tiles = (P4 + 63) / 64;
+    DLS_REQUIRE(tiles < (int64_t)1 << 31, DLS_EINVAL, "dls_subset_fedavg_union_f32: grid too large");
+    const int waves = (S + kSubsetSB - 1) / kSubsetSB;
+    hipLaunchKernelGGL((k_subset_union<kSubsetSB, kSubsetUB>), dim3((unsigned)tiles),
+                       dim3(64 * waves), 0, as_stream(stream), reinterpret_cast<const f32x4 *>(U),
+                       ldu / 4, urows, uweight, member, (int)Ku, sub_total, (int)S, P4,
+                       reinterpret_cast<f32x4 *>(out), ldo / 4);
+    return check_launch("dls_subset_fedavg_union_f32");
 }

@@ -16,18 +16,9 @@ namespace dls {
 namespace {
 
 constexpr int kBlock = 256;
-#ifndef DLS_QUANT_U
-#define DLS_QUANT_U 2  // clients per batch; two batches in flight per lane
-#endif
-#ifndef DLS_QUANT_UG
-#define DLS_QUANT_UG 1  // clients per batch on multi-KiB tiles
-#endif
-#ifndef DLS_QUANT_FORK
-#define DLS_QUANT_FORK 1  // small tile groups on a side stream: 0 off, 1 before the bulk, 2 after
-#endif
-#ifndef DLS_QUANT_SCHED
-#define DLS_QUANT_SCHED 2  // element pairs between scheduling barriers (0: none)
-#endif
+constexpr int kQuantU = 2;      // clients per batch (1 KiB tiles); two batches in flight per lane
+constexpr int kQuantUG = 1;     // clients per batch on multi-KiB tiles
+constexpr int kQuantSched = 2;  // element pairs between scheduling barriers
 
 __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
     return (float)((w >> (8 * k)) & 0xffu);  // selects v_cvt_f32_ubyte{k}
@@ -155,11 +146,9 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
         const f32x2 r = f32x2{acc[j], acc[j + 1]} + q;
         acc[j] = r.x;
         acc[j + 1] = r.y;
-#if DLS_QUANT_SCHED > 0
         // keep the scheduler from widening the chain over all 16 elements of
         // every in-flight client (that costs ~60 VGPRs and waves per SIMD)
-        if ((j / 2) % DLS_QUANT_SCHED == DLS_QUANT_SCHED - 1) __builtin_amdgcn_sched_barrier(0);
-#endif
+        if ((j / 2) % kQuantSched == kQuantSched - 1) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -200,7 +189,7 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8
         auto run = [&](auto common_only, auto g0, auto gn) {
             constexpr bool COMMON = decltype(common_only)::value;
             constexpr int G0 = decltype(g0)::value, GN = decltype(gn)::value;
-            constexpr int U = GN > 1 ? DLS_QUANT_UG : DLS_QUANT_U;  // clients per batch
+            constexpr int U = GN > 1 ? kQuantUG : kQuantU;  // clients per batch
             auto fetch = [&](int j, u32x4 (&qv)[GN], float &sc, float &zz, float &wk) {
                 const int64_t r = readlane_i(tr, j);
                 // wave-uniform row base in a buffer descriptor (SALU), lane offset in
@@ -321,7 +310,7 @@ __device__ __forceinline__ void int_lane_pipelined(float (&acc)[16], const uint8
                                                    SzLayout L, const int32_t *__restrict__ rows,
                                                    const float *__restrict__ w, int K,
                                                    const FastDiv &d) {
-    constexpr int U = DLS_QUANT_U;
+    constexpr int U = kQuantU;
     struct Batch {
         u32x4 qv[U];
         f32x2 sz[U];
@@ -501,11 +490,8 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
     }
 }
 
-#ifndef DLS_QUANT_MINB
-#define DLS_QUANT_MINB 1
-#endif
 template <int G, bool TWO>
-__global__ __launch_bounds__(kBlock, DLS_QUANT_MINB) void k_dequant_fast(
+__global__ __launch_bounds__(kBlock, 1) void k_dequant_fast(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
     const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
@@ -655,9 +641,11 @@ __global__ __launch_bounds__(kBlock) void k_segment_minmax(const float *__restri
         }
     } else {  // chunk crosses segment boundaries (at most nseg such chunks)
         for (int64_t e = c0 + threadIdx.x; e < c1; e += kBlock) {
+            const float v = x[e];
+            if (v != v) continue;  // NaNs are ignored, as fminf / fmaxf do on the bulk path
             const int s = find_segment(seg_off, nseg, e);
-            atomic_min_f32(mins + s, x[e]);
-            atomic_max_f32(maxs + s, x[e]);
+            atomic_min_f32(mins + s, v);
+            atomic_max_f32(maxs + s, v);
         }
     }
 }
@@ -757,10 +745,8 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     DLS_REQUIRE(ldq < ((int64_t)1 << 32), DLS_ELAYOUT,
                 "dls_dequant_fedavg: ldq=%lld must be < 2^32 (32-bit lane offsets)",
                 (long long)ldq);
-#ifndef DLS_QUANT_TWO
-#define DLS_QUANT_TWO 1  // two-constant division when proven exact for N (0: always Markstein)
-#endif
-    const FastDiv d = DLS_QUANT_TWO ? make_fastdiv2(total) : make_fastdiv(total);
+    // two-constant division when proven exact for this N, else Markstein
+    const FastDiv d = make_fastdiv2(total);
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
@@ -780,8 +766,8 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     const int64_t small_tiles = nf - (big >= 0 ? nfast[big] : 0) + ngen;
     hipStream_t side = st;
     hipEvent_t fork = nullptr, join = nullptr;
-    if (DLS_QUANT_FORK && big >= 0 && small_tiles > 0) {
-        hipStream_t s2 = side_stream();
+    if (big >= 0 && small_tiles > 0) {
+        hipStream_t s2 = side_stream(st);
         if (s2 && hipEventCreateWithFlags(&fork, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&join, hipEventDisableTiming) == hipSuccess &&
             hipEventRecord(fork, st) == hipSuccess && hipStreamWaitEvent(s2, fork, 0) == hipSuccess)
@@ -801,7 +787,6 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
                            reinterpret_cast<const uint8_t *>(Q), ldq,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
     };
-    if (DLS_QUANT_FORK == 2 && big >= 0) launch_fast(big, st);
     for (int g = 0; g < 4; ++g)
         if (g != big) launch_fast(g, side);
     if (ngen > 0)
@@ -809,7 +794,7 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
                            dim3(kBlock), 0, side, t, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
-    if (DLS_QUANT_FORK != 2 && big >= 0) launch_fast(big, st);
+    if (big >= 0) launch_fast(big, st);
     int rc = check_launch("dls_dequant_fedavg");
     if (side != st) {
         hipError_t e = hipEventRecord(join, side);

@@ -10,8 +10,6 @@
 // (Harley-Seal) adder tree, so 8 clients cost 7 CSAs (5 bitwise ops each)
 // per plane word and no per-parameter unpacking; the counters are unpacked
 // once at the end.  Exact in any order.
-#include <type_traits>
-
 #include "dls_common.h"
 
 namespace dls {
@@ -58,10 +56,7 @@ __device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *
 
 // grid: x = blocks of 4 waves x kPackTPW tiles, y = client.  Each wave issues
 // the loads of its kPackTPW tiles before packing any (memory-level parallelism).
-#ifndef DLS_PACK_TPW
-#define DLS_PACK_TPW 4
-#endif
-constexpr int kPackTPW = DLS_PACK_TPW;
+constexpr int kPackTPW = 4;
 
 __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ X, int64_t ldx,
                                                       int64_t P, uint64_t *__restrict__ planes,
@@ -94,44 +89,10 @@ __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ 
 // are carry-save partial counts, every 8 inputs emit an "eights" word that
 // ripples into the CB-bit counter c (in units of 8).  7 CSAs of 5 ops per 8
 // clients instead of 8 ripple increments of 2*B ops.
-// A/B knob DLS_VOTE_BITOP3: gfx950's three-input v_bitop3_b32 (truth table over
-// src0 = 0xf0, src1 = 0xcc, src2 = 0xaa) makes a carry-save adder two VALU ops
-// per 32-bit half, l = a ^ b ^ c (0x96) and h = maj(a, b, c) (0xe8): 37 % fewer
-// VALU in the vote loop, yet measured 6 % slower at K = 1000 (0.475 vs 0.447 ms,
-// v_bfi form 0.463): the vote is not VALU-bound, so the plain form stays.
-template <int T>
-__device__ __forceinline__ uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
-    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, T);
-    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32),
-                                                    (uint32_t)(c >> 32), T);
-    return ((uint64_t)hi << 32) | lo;
-}
-[[maybe_unused]] constexpr int kXor3 = 0x96;
-[[maybe_unused]] constexpr int kMaj = 0xe8;
-[[maybe_unused]] constexpr int kAndOr = 0xea;  // (src0 & src1) | src2
-
-#ifndef DLS_VOTE_BITOP3
-#define DLS_VOTE_BITOP3 0  // 1: v_bitop3, 2: v_bfi (measured slower: A/B knob)
-#endif
 __device__ __forceinline__ void csa(uint64_t &h, uint64_t &l, uint64_t a, uint64_t b, uint64_t c) {
-#if DLS_VOTE_BITOP3 == 1
-    h = bitop3_64<kMaj>(a, b, c);
-    l = bitop3_64<kXor3>(a, b, c);
-#elif DLS_VOTE_BITOP3 == 2
-    // xor, xor, v_bfi_b32 (maj = bfi(a ^ b, c, a)) per half
-    const uint64_t u = a ^ b;
-    l = u ^ c;
-    uint32_t hl, hh;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hl) : "v"((uint32_t)u), "v"((uint32_t)c), "v"((uint32_t)a));
-    asm("v_bfi_b32 %0, %1, %2, %3"
-        : "=v"(hh)
-        : "v"((uint32_t)(u >> 32)), "v"((uint32_t)(c >> 32)), "v"((uint32_t)(a >> 32)));
-    h = ((uint64_t)hh << 32) | hl;
-#else
     const uint64_t u = a ^ b;
     h = (a & b) | (u & c);
     l = u ^ c;
-#endif
 }
 
 template <int CB>
@@ -152,35 +113,7 @@ struct HSCounter {
         csa(twosB, ones, ones, x[6], x[7]);
         csa(foursB, twos, twos, twosA, twosB);
         csa(eights, fours, fours, foursA, foursB);
-#pragma unroll
-        for (int b = 0; b < CB; ++b) {  // c += eights (bit-sliced ripple)
-            const uint64_t t = c[b] & eights;
-            c[b] ^= eights;
-            eights = t;
-        }
-    }
-    // Half batches of 4 clients: phase 0 leaves its fours word pending, phase 1
-    // combines it with its own into an eights word (same carry-save sums as add8).
-    uint64_t fpend = 0;
-    template <int PHASE>
-    __device__ __forceinline__ void add4(const uint64_t (&x)[4]) {
-        uint64_t twosA, twosB, fnew;
-        csa(twosA, ones, ones, x[0], x[1]);
-        csa(twosB, ones, ones, x[2], x[3]);
-        csa(fnew, twos, twos, twosA, twosB);
-        if (PHASE == 0) {
-            fpend = fnew;
-        } else {
-            uint64_t eights;
-            csa(eights, fours, fours, fpend, fnew);
-            ripple(eights);
-        }
-    }
-    __device__ __forceinline__ void flush4() {  // after an odd number of half batches
-        const uint64_t eights = fours & fpend;
-        fours ^= fpend;
-        fpend = 0;
-        ripple(eights);
+        ripple(eights);  // c += eights
     }
     __device__ __forceinline__ void ripple(uint64_t eights) {
 #pragma unroll
@@ -210,15 +143,8 @@ struct HSCounter {
 // the wave writes its 4096 outputs coalesced, a 16-lane group per 64-parameter
 // group, instead of 64 lanes each scattering 256 bytes.
 constexpr int kVoteBlock = 64;
-#ifndef DLS_VOTE_G
-#define DLS_VOTE_G 4  // groups per lane on large models (each wave streams G KB per client)
-#endif
-#ifndef DLS_VOTE_HALF
-#define DLS_VOTE_HALF 0  // 1: 4-client half batches double-buffered on the widest waves
-#endif
-#ifndef DLS_VOTE_DBG
-#define DLS_VOTE_DBG 1  // widest G whose 8-client batches are double-buffered
-#endif
+constexpr int kVoteG = 4;    // groups per lane on large models (each wave streams G KB per client)
+constexpr int kVoteDbG = 1;  // widest G whose 8-client batches are double-buffered
 
 
 template <int CB, bool ROWS, int G>
@@ -251,11 +177,7 @@ __device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes,
             for (int u = 0; u < B8; ++u) {
                 xp[u] = w8[q][u][0];
                 xn[u] = w8[q][u][1];
-#if DLS_VOTE_BITOP3 == 1
-                nan[q] = bitop3_64<kAndOr>(xp[u], xn[u], nan[q]);
-#else
                 nan[q] |= xp[u] & xn[u];
-#endif
             }
             cp[q].add8(xp);
             cn[q].add8(xn);
@@ -264,82 +186,7 @@ __device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes,
     // batches of 8 clients, double-buffered; loads inside the steady-state loop
     // are unconditional so every consume waits with an exact vmcnt
     const int nb = K / B8;
-    if (DLS_VOTE_HALF && G > DLS_VOTE_DBG) {
-        // half batches (4 clients x G KB) double-buffered: the same registers as
-        // one 8-client batch, but a batch's loads fly while the other is reduced
-        constexpr int B4 = 4;
-        auto load4 = [&](int j, u64x2 (&w4)[G][B4]) {
-#pragma unroll
-            for (int u = 0; u < B4; ++u) {
-                const u64x2 *r = base + row(j + u) * ldp2;
-#pragma unroll
-                for (int q = 0; q < G; ++q) w4[q][u] = __builtin_nontemporal_load(r + qoff[q]);
-            }
-        };
-        auto consume4 = [&](const u64x2 (&w4)[G][B4], auto phase) {
-            constexpr int PH = decltype(phase)::value;
-#pragma unroll
-            for (int q = 0; q < G; ++q) {
-                uint64_t xp[B4], xn[B4];
-#pragma unroll
-                for (int u = 0; u < B4; ++u) {
-                    xp[u] = w4[q][u][0];
-                    xn[u] = w4[q][u][1];
-                    nan[q] |= xp[u] & xn[u];
-                }
-                cp[q].template add4<PH>(xp);
-                cn[q].template add4<PH>(xn);
-            }
-        };
-        using Ph0 = std::integral_constant<int, 0>;
-        using Ph1 = std::integral_constant<int, 1>;
-        const int nh = K / B4;
-        if (nh > 0) {
-            u64x2 wa[G][B4], wb[G][B4];
-            load4(0, wa);
-            int b = 0;
-            for (; b + 2 < nh; b += 2) {
-                load4((b + 1) * B4, wb);
-                __builtin_amdgcn_sched_barrier(0);
-                consume4(wa, Ph0{});
-                __builtin_amdgcn_sched_barrier(0);
-                load4((b + 2) * B4, wa);
-                __builtin_amdgcn_sched_barrier(0);
-                consume4(wb, Ph1{});
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (b + 1 < nh) {
-                load4((b + 1) * B4, wb);
-                consume4(wa, Ph0{});
-                consume4(wb, Ph1{});
-            } else {
-                consume4(wa, Ph0{});
-#pragma unroll
-                for (int q = 0; q < G; ++q) {
-                    cp[q].flush4();
-                    cn[q].flush4();
-                }
-            }
-        }
-        if (nh * B4 < K) {  // tail: missing clients count as zero planes
-            u64x2 w4[G][B4];
-#pragma unroll
-            for (int u = 0; u < B4; ++u) {
-                const int k = nh * B4 + u;
-#pragma unroll
-                for (int q = 0; q < G; ++q)
-                    w4[q][u] = k < K ? __builtin_nontemporal_load(base + row(k) * ldp2 + qoff[q]) : u64x2{0, 0};
-            }
-            consume4(w4, Ph0{});
-#pragma unroll
-            for (int q = 0; q < G; ++q) {
-                cp[q].flush4();
-                cn[q].flush4();
-            }
-        }
-        return;
-    }
-    if (G > DLS_VOTE_DBG) {  // one batch (8 clients x G KB) in flight per wave: register budget
+    if (G > kVoteDbG) {  // one batch (8 clients x G KB) in flight per wave: register budget
         for (int b = 0; b < nb; ++b) {
             u64x2 wa[G][B8];
             load8(b * B8, wa);
@@ -616,7 +463,7 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
     // 4 groups per lane (each wave streams 4 KB of every client row, measured
     // 12 % faster than 1 KB at P = 11.2M) while that still leaves >= 2 waves per
     // CU; 1 group per lane (double-buffered batches) for small models
-    constexpr int GW = DLS_VOTE_G;
+    constexpr int GW = kVoteG;
     const bool wide = CB <= 12 && (vote_groups + 64 * GW - 1) / (64 * GW) >= 512;
     const dim3 grid((unsigned)(wide ? (vote_groups + 64 * GW - 1) / (64 * GW) : (vote_groups + 63) / 64));
 #define DLS_VOTE_LAUNCH(C_, G_)                                                              \

@@ -235,6 +235,10 @@ class _ShardedShapleyMixin(_ShardedMixin):
     def _before_aggregate(self):
         self._gather_clients()
 
+    @property
+    def store_capacity(self):
+        return self.worker_number  # every rank ends the round holding all K client rows
+
 
 def _sharded_shapley(cls):
     class Sharded(_ShardedShapleyMixin, cls):

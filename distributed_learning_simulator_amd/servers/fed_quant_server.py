@@ -41,7 +41,7 @@ class FedQuantServer(FedServer):
         self.last_aggregate = None
 
     def _make_store(self, payload):
-        return QuantizedClientStore(payload, self.device, capacity=self.worker_number)
+        return QuantizedClientStore(payload, self.device, capacity=self.store_capacity)
 
     def _process_client_parameter(self, client_parameter: dict):
         # The int payload is stored as-is; dequantization is fused into the

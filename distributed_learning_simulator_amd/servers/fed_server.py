@@ -37,9 +37,16 @@ class FedServer(Server):
         the sharded servers in ``distributed.py`` override it)."""
         return self.worker_number
 
+    @property
+    def store_capacity(self):
+        """Client rows this process holds per round: its own clients (the sharded
+        servers receive only their local ones; the sharded Shapley servers
+        override this, they all-gather every client)."""
+        return self.clients_per_round
+
     def _make_store(self, parameter_dict):
         return ClientUpdateStore(ParameterLayout.from_dict(parameter_dict), self.device,
-                                 capacity=self.worker_number)
+                                 capacity=self.store_capacity)
 
     def get_metric(self, model, metric_type="acc"):
         """servers/fed_server.py:26-32 — load, run the tester, top-1 accuracy or loss."""
@@ -98,4 +105,5 @@ class FedServer(Server):
         acc = self.get_metric(self.prev_model)
         log.info("end aggregating, test accuracy is %s", acc)
         self.parameters.clear()
-        return RepeatedResult(data=data, num=self.worker_number)
+        # one copy per client that feeds this process (its local clients when sharded)
+        return RepeatedResult(data=data, num=self.clients_per_round)

@@ -87,6 +87,26 @@ int dls_subset_fedavg_f32(const float *U, int64_t ldu, const int32_t *sub_off,
                           const float *sub_total, int32_t S, int64_t P, float *out,
                           int64_t ldo, dls_stream_t stream);
 
+/* The same batch, reading each client row ONCE (the Shapley servers' default
+ * path: servers/GTG_shapley_value_server.py:56 and
+ * servers/multiround_shapley_value_server.py:37 call get_subset_model,
+ * servers/fed_server.py:44-66, once per coalition; a batch's coalitions share
+ * their clients).
+ *   urows   int32 [Ku]   row of U of each client of the batch's union
+ *   uweight fp32  [Ku]   fl32(n_j)
+ *   member  uint64 [Ku]  bit s set iff client j belongs to coalition s
+ *   sub_total fp32 [S]   fl32(N_s) of coalition s; S <= DLS_SUBSET_UNION_MAX
+ * Row s of out [S, ldo] is coalition s's weighted mean, its members summed in
+ * union order: bit-exact with the reference when every coalition lists its
+ * clients in the union's order (the caller orders the union so — sorted
+ * worker-id tuples, as the Shapley servers pass them, always are).  A coalition
+ * without members leaves its row undefined. */
+#define DLS_SUBSET_UNION_MAX 64
+int dls_subset_fedavg_union_f32(const float *U, int64_t ldu, const int32_t *urows,
+                                const float *uweight, const uint64_t *member, int32_t Ku,
+                                const float *sub_total, int32_t S, int64_t P, float *out,
+                                int64_t ldo, dls_stream_t stream);
+
 /* Subset aggregation as a dense fp32 MFMA contraction: out[S, P] = C[S, K] · U[rows, P]
  * (C row-major [S, K], c_si = n_i / N_S; rows[K] selects the K client rows of U).
  * fp32 in / fp32 accumulate (v_mfma_f32_32x32x2_f32): an fma chain in client

@@ -42,6 +42,18 @@ def subset_fedavg(U, sub_off, sub_rows, sub_weight, sub_total, P, out, stream=No
     return out
 
 
+def subset_fedavg_union(U, urows, uweight, member, sub_total, P, out, stream=None):
+    rows = _f32(urows).astype(np.int64)
+    w = _f32(uweight)
+    m = _f32(member).view(np.uint64)
+    tot = _f32(sub_total)
+    for s in range(tot.size):
+        sel = [j for j in range(rows.size) if (int(m[j]) >> s) & 1]
+        fedavg(U, torch.from_numpy(rows[sel].astype(np.int32)),
+               torch.from_numpy(w[sel].copy()), float(tot[s]), P, out[s])
+    return out
+
+
 def subset_gemm(C, U, rows, P, out, stream=None):
     Cn = _f32(C).astype(np.float64)
     Un = _f32(U)[_f32(rows).astype(np.int64), :P].astype(np.float64)
@@ -89,14 +101,14 @@ def sign_vote(planes, rows, K, P, sign_out, counts=None, vote_planes=None, strea
 
 def install(monkeypatch):
     monkeypatch.setattr(_native, "require_gpu", lambda: None)
-    for name in ("fedavg", "subset_fedavg", "subset_gemm", "sign_pack", "sign_vote_count",
-                 "sign_from_counts", "sign_vote"):
+    for name in ("fedavg", "subset_fedavg", "subset_fedavg_union", "subset_gemm", "sign_pack",
+                 "sign_vote_count", "sign_from_counts", "sign_vote"):
         monkeypatch.setattr(_native, name, globals()[name])
 
 
 def install_global():
     """Same as install() for spawned processes (no pytest monkeypatch there)."""
     _native.require_gpu = lambda: None
-    for name in ("fedavg", "subset_fedavg", "subset_gemm", "sign_pack", "sign_vote_count",
-                 "sign_from_counts", "sign_vote"):
+    for name in ("fedavg", "subset_fedavg", "subset_fedavg_union", "subset_gemm", "sign_pack",
+                 "sign_vote_count", "sign_from_counts", "sign_vote"):
         setattr(_native, name, globals()[name])

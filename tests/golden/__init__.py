@@ -31,3 +31,23 @@ def split(flat, layout):
         out[name] = np.asarray(flat[off:off + m]).reshape(shape)
         off += m
     return out
+
+
+def shapley_large_cases():
+    """GTG N=50 / multiround N=12 (shapley_large.npz) in the shapley_cases() form;
+    'evaluated' as sorted tuples decoded from the stored bit masks."""
+    z = load("shapley_large.npz")
+    cases = []
+    for m in meta(z):
+        t = m["tag"]
+        K = m["K"]
+        case = dict(m)
+        case.update(U=z[f"{t}_U"], n=[int(x) for x in z[f"{t}_n"]], prev=z[f"{t}_prev"],
+                    target=z[f"{t}_target"],
+                    sv={str(i): float(v) for i, v in enumerate(z[f"{t}_sv"])},
+                    evaluated=[tuple(i for i in range(K) if (int(b) >> i) & 1)
+                               for b in z[f"{t}_evaluated"]],
+                    metric_pickle=(z[f"{t}_metric_pickle"].tobytes()
+                                   if f"{t}_metric_pickle" in z.files else None))
+        cases.append(case)
+    return cases

@@ -394,15 +394,21 @@ def run_shapley(cls, layout, K, seed, tag):
 
     server.get_subset_model = spy
     np.random.seed(seed)
+    metric_pickle = None
     with tempfile.TemporaryDirectory() as td, contextlib.chdir(td) if hasattr(contextlib, "chdir") else _cd(td):
         for i in range(K):
             server._process_worker_data((i, n[i], unflat(U[i], layout)), None)
+        if os.path.exists("metric_1"):  # multiround's side effect (:56-57), byte for byte
+            with open("metric_1", "rb") as f:
+                metric_pickle = f.read()
     sv = server.shapley_values[1]
+    assert any(float(v) != 0.0 for v in sv.values()), "round truncated: choose other clients"
     return {
         "tag": tag, "K": K, "seed": seed, "U": U.tolist(), "n": n, "prev": prev.tolist(),
         "target": target.tolist(), "scale": scale, "layout": layout,
         "sv": {str(k): float(v) for k, v in sv.items()},
         "evaluated": evaluated[1:],  # [0] is the round's full aggregation
+        "metric_pickle_hex": metric_pickle.hex() if metric_pickle is not None else None,
     }
 
 
@@ -416,8 +422,11 @@ def _cd(path):
         os.chdir(old)
 
 
+SHAPLEY_LAYOUT = [("w", (6, 5)), ("b", (6,)), ("v", (11,))]
+
+
 def gen_shapley():
-    layout = [("w", (6, 5)), ("b", (6,)), ("v", (11,))]
+    layout = SHAPLEY_LAYOUT
     cases = []
     for K in (3, 4, 6):
         cases.append(run_shapley(MultiRoundShapleyValueServer, layout, K, 0, f"multiround_{K}"))
@@ -425,6 +434,31 @@ def gen_shapley():
         cases.append(run_shapley(GTGShapleyValueServer, layout, K, seed, f"gtg_{K}_{seed}"))
     with open(os.path.join(HERE, "shapley.json"), "w") as f:
         json.dump(cases, f)
+
+
+def gen_shapley_large():
+    """BASELINE config 5 at its stated client count: GTG at N = 50 (~4.5k
+    coalitions) and multiround at N = 12 (all 4,096), on the small layout with
+    the deterministic utility.  Stored compactly: coalitions as uint64 bit masks
+    in evaluation order, the multiround metric_1 pickle as raw bytes."""
+    out, cases = {}, []
+    for cls, K, seed, tag in ((GTGShapleyValueServer, 50, 4, "gtg_50_4"),
+                              (MultiRoundShapleyValueServer, 12, 0, "multiround_12")):
+        c = run_shapley(cls, SHAPLEY_LAYOUT, K, seed, tag)
+        out[f"{tag}_U"] = np.array(c["U"], np.float32)
+        out[f"{tag}_n"] = np.array(c["n"], np.int64)
+        out[f"{tag}_prev"] = np.array(c["prev"], np.float32)
+        out[f"{tag}_target"] = np.array(c["target"], np.float64)
+        out[f"{tag}_sv"] = np.array([c["sv"][str(i)] for i in range(K)], np.float64)
+        out[f"{tag}_evaluated"] = np.array(
+            [sum(1 << i for i in s) for s in c["evaluated"]], np.uint64)
+        if c["metric_pickle_hex"] is not None:
+            out[f"{tag}_metric_pickle"] = np.frombuffer(bytes.fromhex(c["metric_pickle_hex"]),
+                                                        np.uint8)
+        cases.append({"tag": tag, "K": K, "seed": seed, "scale": c["scale"],
+                      "layout": SHAPLEY_LAYOUT, "n_evaluated": len(c["evaluated"])})
+    out["meta"] = np.array(json.dumps(cases))
+    np.savez_compressed(os.path.join(HERE, "shapley_large.npz"), **out)
 
 
 if __name__ == "__main__":
@@ -435,6 +469,7 @@ if __name__ == "__main__":
     gen_dequant()
     gen_quantize()
     gen_shapley()
+    gen_shapley_large()
     for f in sorted(os.listdir(HERE)):
         if f.endswith((".npz", ".json")):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -42,14 +42,24 @@ def _fedavg_worker(rank, world, port, outq):
     U, n = z[f"{k}_U"], z[f"{k}_n"]
     server = ShardedFedServer(tester=None, worker_number=K, synchronous=True,
                               device=torch.device("cpu"), chunks=3)
-    for wid in server.local_worker_ids:
-        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
-        server.worker_data_queue.add_task((wid, int(n[wid]), d))
-    for w in server.local_worker_ids:
-        server.worker_data_queue.get_result(consumer=w, timeout=30)
-    res = server.worker_data_queue.get_result(consumer=server.local_worker_ids[0], timeout=30)
-    outq.put((rank, server.local_worker_ids,
-              np.concatenate([res[nm].reshape(-1).numpy() for nm, _ in layout])))
+    q = server.worker_data_queue
+    local = server.local_worker_ids
+    for w in local:  # the initial broadcast, once per local worker
+        q.get_result(consumer=w, timeout=30)
+    assert len(q._results) == 0
+    flats = []
+    for _round in range(3):  # every round's broadcast is retired once each local worker took it
+        for wid in local:
+            d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
+            q.add_task((wid, int(n[wid]), d))
+        # a rank stores only its own clients' rows, not the global K
+        assert server.parameters.store.capacity == len(local)
+        for w in local:
+            res = q.get_result(consumer=w, timeout=30)
+        assert len(q._results) == 0, "round result left in the queue"
+        flats.append(np.concatenate([res[nm].reshape(-1).numpy() for nm, _ in layout]))
+    assert all(np.array_equal(f.view(np.uint32), flats[0].view(np.uint32)) for f in flats)
+    outq.put((rank, local, flats[0]))
     dist.destroy_process_group()
 
 

@@ -163,3 +163,125 @@ def test_fed_server_round_golden():
     res = server.worker_data_queue.get_result(consumer=0)
     flat = np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout])
     assert same_bits(flat, z[f"{k}_full"])
+
+
+def _union(Ud, n, subsets, P=None):
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.aggregation import union_batch
+    P = P or Ud.shape[1]
+    t = union_batch(subsets, {i: int(n[i]) for i in range(len(n))}, dev)
+    assert t is not None
+    out = torch.full((len(subsets), P), float("nan"), device=dev)
+    _native.subset_fedavg_union(Ud, *t, P, out)
+    return out
+
+
+@pytest.mark.parametrize("S", [1, 9, 17, 64])
+def test_subset_union_bit_exact(S):
+    """dls_subset_fedavg_union_f32 (every client row read once per batch) vs the
+    reference op order, per coalition: rows in arbitrary order, > 64 clients
+    (two table chunks), a ragged last tile, and special values that send some
+    tiles down the redo path (zeros, denormals, huge, inf, nan)."""
+    K, P = 70, 4096 * 3 + 12
+    g = torch.Generator().manual_seed(S)
+    U = (torch.randn(K, P, generator=g) * 0.05).numpy()
+    U[3, :8] = [0.0, -0.0, 1e-40, -1e-39, 3e38, np.inf, np.nan, 1e-45]
+    U[:, 600:604] = 0.0  # a column of zeros in every client: -0 / +0 sums
+    U[7, 5000] = -0.0
+    n = [int(x) for x in torch.randint(1, 1001, (K,), generator=g)]
+    perm = torch.randperm(K, generator=g).tolist()  # worker -> row
+    subsets = []
+    for s in range(S):
+        k = int(torch.randint(1, K + 1, (1,), generator=g))
+        members = sorted(torch.randperm(K, generator=g)[:k].tolist())
+        subsets.append([perm[w] for w in members])
+    subsets[0] = [perm[w] for w in range(K)]
+    got = _union(torch.from_numpy(U).to(dev), n, subsets).cpu().numpy()
+    for s, sub in enumerate(subsets):
+        assert same_bits(got[s], _c.fedavg_ref(U, n, sub)), s
+
+
+def test_subset_union_through_shapley_store():
+    """ClientUpdateStore.subset_models takes the union kernel for sorted coalitions."""
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.aggregation import ClientUpdateStore
+    from distributed_learning_simulator_amd.layout import ParameterLayout
+    calls = []
+    orig = _native.subset_fedavg_union
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    lay = ParameterLayout([("w", (33, 31)), ("b", (5,))])
+    st = ClientUpdateStore(lay, dev, capacity=12)
+    g = torch.Generator().manual_seed(7)
+    rows = [st.acquire() for _ in range(12)]
+    for r in rows:
+        st.write(r, {"w": torch.randn(33, 31, generator=g), "b": torch.randn(5, generator=g)})
+    n = {r: 50 + 13 * r for r in rows}
+    subs = [[rows[i] for i in sorted(torch.randperm(12, generator=g)[:1 + s % 12].tolist())]
+            for s in range(70)]  # 70 coalitions: two union launches (64 + 6)
+    _native.subset_fedavg_union = spy
+    try:
+        out = st.subset_models(subs, n).cpu().numpy()
+    finally:
+        _native.subset_fedavg_union = orig
+    assert len(calls) == 2
+    U = st.U.cpu().numpy()
+    nn = [n.get(i, 1) for i in range(U.shape[0])]
+    for s, sub in enumerate(subs):
+        assert same_bits(out[s], _c.fedavg_ref(U, nn, sub)), s
+
+
+def test_config5_scale_subset_kernels_resnet18():
+    """BASELINE config 5 at its stated scale: 50 clients x full ResNet-18, S = 50
+    GTG-like coalitions (sorted prefixes of random permutations).  Both exact
+    kernels (union and per-coalition) bit-exact vs the oracle on 64Ki sampled
+    parameters of every coalition; the fp32 MFMA GEMM normwise <= 1e-6 vs fp64."""
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.layout import ParameterLayout
+    from distributed_learning_simulator_amd.model_shapes import resnet18_cifar
+    lay = ParameterLayout(resnet18_cifar())
+    K, S, P = 50, 50, lay.P
+    g = torch.Generator(device=dev).manual_seed(20250131)
+    Ud = torch.empty((K, P), device=dev).normal_(generator=g).mul_(0.05)
+    gc = torch.Generator().manual_seed(5)
+    n = [int(x) for x in torch.randint(100, 1001, (K,), generator=gc)]
+    subsets = []
+    for s in range(S):
+        perm = torch.randperm(K, generator=gc).tolist()
+        subsets.append(sorted(perm[: 1 + (s * 7) % K]))
+    cols = torch.sort(torch.randperm(lay.numel, generator=gc)[:1 << 16]).values
+    cols_d = cols.to(dev)
+    Uc = Ud[:, cols_d].cpu().numpy()
+    # union kernel (the Shapley servers' default)
+    got = _union(Ud, n, subsets)[:, cols_d].cpu().numpy()
+    for s, sub in enumerate(subsets):
+        assert same_bits(got[s], _c.fedavg_ref(Uc, n, sub)), ("union", s)
+    # per-coalition kernel (dls_subset_fedavg_f32)
+    off, rows, w, tot = [0], [], [], []
+    for sub in subsets:
+        rows += sub
+        w += [n[r] for r in sub]
+        tot.append(float(sum(n[r] for r in sub)))
+        off.append(len(rows))
+    out = torch.empty((S, P), device=dev)
+    _native.subset_fedavg(Ud, torch.tensor(off, dtype=torch.int32, device=dev),
+                          torch.tensor(rows, dtype=torch.int32, device=dev),
+                          torch.tensor(w, dtype=torch.float32, device=dev),
+                          torch.tensor(tot, dtype=torch.float32, device=dev), P, out)
+    got = out[:, cols_d].cpu().numpy()
+    for s, sub in enumerate(subsets):
+        assert same_bits(got[s], _c.fedavg_ref(Uc, n, sub)), ("per-coalition", s)
+    # MFMA contraction
+    C = torch.zeros((S, K), dtype=torch.float64)
+    for s, sub in enumerate(subsets):
+        for r in sub:
+            C[s, r] = n[r] / sum(n[i] for i in sub)
+    _native.subset_gemm(C.float().to(dev), Ud, torch.arange(K, dtype=torch.int32, device=dev), P,
+                        out)
+    got = out[:, cols_d].cpu().double()
+    ref = C @ torch.from_numpy(Uc).double()
+    err = torch.linalg.norm(got - ref, dim=1) / torch.linalg.norm(ref, dim=1)
+    assert float(err.max()) < 1e-6, float(err.max())

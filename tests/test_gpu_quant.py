@@ -306,3 +306,55 @@ def test_dequant_fedavg_full_vgg16_sampled_channels():
             got.append(out[name].reshape(-1).cpu().numpy())
     ref = oquant.dequant_fedavg(clients, n, order, layout)
     assert same_bits(np.concatenate(got), ref)
+
+
+def test_int8_symmetric_per_channel_quantize_golden():
+    """The fed_quant worker's device path (workers/fed_quant_worker.py): int8
+    (qmin = -128) per-channel quantize vs torch.quantize_per_channel's ints in
+    quantize.npz (pc_*), and symmetric qparams vs torch.ao's per-channel
+    symmetric MinMax observer (fp32 scale, zero point 0)."""
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.workers.fed_quant_worker import \
+        quantize_per_channel_symmetric
+    z = G.load("quantize.npz")
+    x = torch.from_numpy(z["pc_x"].copy())
+    C = x.shape[0]
+    row = x[0].numel()
+    seg = (torch.arange(C + 1, dtype=torch.int64) * row).to(dev)
+    scale = torch.from_numpy(z["pc_scale"].astype(np.float32)).to(dev)
+    zp = torch.zeros(C, dtype=torch.int32, device=dev)
+    q = torch.empty(x.numel(), dtype=torch.int8, device=dev)
+    deq = torch.empty(x.numel(), device=dev)
+    _native.quantize(x.reshape(-1).to(dev), seg, x.numel(), scale, zp, q, deq, qmin=-128, qmax=127)
+    assert np.array_equal(q.cpu().numpy().reshape(z["pc_q"].shape), z["pc_q"])
+    ref_deq = (z["pc_q"].astype(np.float32) * z["pc_scale"].astype(np.float32)[:, None, None])
+    assert same_bits(deq.cpu().numpy(), ref_deq.reshape(-1))
+    # the worker's whole chain: segment min/max -> symmetric qparams -> quantize
+    obs = torch.ao.quantization.PerChannelMinMaxObserver(
+        ch_axis=0, dtype=torch.qint8, qscheme=torch.per_channel_symmetric)
+    obs(x)
+    sc_ref, zp_ref = obs.calculate_qparams()
+    qw, sc, zpw = quantize_per_channel_symmetric(x.to(dev))
+    assert np.array_equal(sc.cpu().numpy(), sc_ref.float().numpy())
+    assert np.array_equal(zpw.cpu().numpy(), zp_ref.int().numpy())
+    qt = torch.quantize_per_channel(x, sc_ref.double(), zp_ref, 0, torch.qint8)
+    assert np.array_equal(qw.cpu().numpy(), qt.int_repr().numpy())
+
+
+def test_segment_minmax_ignores_nan():
+    """NaNs are ignored (dls_hip.h) on both the bulk and the segment-boundary path."""
+    from distributed_learning_simulator_amd import _native
+    sizes = [5, 8190, 3, 9000, 1]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(int(off[-1]), generator=g) + 0.5  # all positive
+    x[off[:-1] + 1 - (np.array(sizes) == 1)] = float("nan")  # one NaN per segment
+    x[8192:8200] = float("nan")  # inside a boundary-crossing chunk
+    x[-1] = 0.75  # the 1-element segment keeps a value
+    mins = torch.empty(len(sizes), device=dev)
+    maxs = torch.empty(len(sizes), device=dev)
+    _native.segment_minmax(x.to(dev), torch.from_numpy(off).to(dev), int(off[-1]), mins, maxs)
+    for s in range(len(sizes)):
+        part = x[off[s]:off[s + 1]]
+        part = part[~torch.isnan(part)]
+        assert float(mins[s]) == float(part.min()) and float(maxs[s]) == float(part.max()), s

@@ -230,3 +230,41 @@ def test_vote_wide_tiles_rows_and_padding():
     assert same_bits(sign.cpu().numpy(), s2.cpu().numpy())
     assert torch.equal(vp, v2)
     assert same_bits(sign.cpu().numpy(), osign.majority_vote(S))
+
+
+def test_vote_signs_packed_1000_clients_resnet18_every_parameter():
+    """The instance SignSGDServer and bench.py launch at config 3 (signs + packed
+    vote, no counts: k_sign_vote<8, false, 4>) at full size, 1000 x ResNet-18:
+    every parameter equal to counts -> sign of the count kernel (<8, true, 4>),
+    and 4,096 sampled parameters equal to the oracle's vote."""
+    from distributed_learning_simulator_amd import _native
+    K, P = 1000, 11173962
+    Pp = (P + 3) // 4 * 4
+    W = _native.sign_words(Pp)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]
+    # ties: two clients' planes mirrored on a band of groups; NaN codes on a few
+    planes[1, 2000:4000:2], planes[1, 2001:4001:2] = planes[0, 2001:4001:2], planes[0, 2000:4000:2]
+    planes[17, 2 * 12345 + 1] |= planes[17, 2 * 12345]
+    planes[:, 2 * (Pp // 64):] = 0  # past P: zero, as the packer leaves it
+    sign = torch.empty(Pp, device=dev)
+    vote = torch.full((W,), 0x55, dtype=torch.int64, device=dev)
+    _native.sign_vote(planes, None, K, Pp, sign, vote_planes=vote)  # the timed launch
+    counts = torch.empty(Pp, dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, None, K, Pp, counts)
+    s2 = torch.empty(Pp, device=dev)
+    v2 = torch.zeros(W, dtype=torch.int64, device=dev)
+    _native.sign_from_counts(counts, Pp, s2, v2)
+    assert torch.equal(sign.view(torch.int32), s2.view(torch.int32))
+    assert torch.equal(vote, v2)
+    idx = torch.randint(0, P, (4096,), generator=g, device=dev)
+    idx[:4] = torch.tensor([64 * 1000 + 3, 64 * 12345 + 5, 64 * 12345 + 63, P - 1], device=dev)
+    words = planes[:, (idx // 64) * 2].cpu().numpy().view(np.uint64)
+    nwords = planes[:, (idx // 64) * 2 + 1].cpu().numpy().view(np.uint64)
+    bit = (idx % 64).cpu().numpy().astype(np.uint64)
+    pos = ((words >> bit) & np.uint64(1)).astype(np.float32)
+    neg = ((nwords >> bit) & np.uint64(1)).astype(np.float32)
+    S = pos - neg
+    S[(pos == 1) & (neg == 1)] = np.nan  # the NaN code
+    assert same_bits(sign[idx].cpu().numpy(), osign.majority_vote(S))

@@ -220,3 +220,86 @@ def test_fastdiv_random_divisors():
     rng = np.random.default_rng(1)
     for b in rng.integers(1, 2**31, size=3):
         assert _c.fastdiv_check(float(np.float32(b))) == 0
+
+
+def test_union_order_topological_merge():
+    """dls_subset_fedavg_union_f32 walks one client order for a whole batch; every
+    coalition's own order must be a subsequence of it (aggregation.union_order)."""
+    from distributed_learning_simulator_amd.aggregation import union_order
+    assert union_order([[0, 2], [1, 2, 5], [0, 1]]) == [0, 1, 2, 5]
+    assert union_order([[3, 1], [1, 0]]) == [3, 1, 0]  # rows need not be sorted
+    assert union_order([[0, 1], [1, 0]]) is None  # contradictory orders
+    assert union_order([[0, 0]]) is None  # a repeated client: per-coalition kernel
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        perm = rng.permutation(40)  # arbitrary worker -> row map, sorted worker tuples
+        subs = [[int(perm[w]) for w in sorted(rng.choice(40, rng.integers(1, 40), replace=False))]
+                for _ in range(64)]
+        order = union_order(subs)
+        pos = {r: i for i, r in enumerate(order)}
+        assert all(all(pos[a] < pos[b] for a, b in zip(s, s[1:])) for s in subs)
+
+
+def test_union_batch_tables():
+    from distributed_learning_simulator_amd.aggregation import union_batch
+    subs = [[4, 2], [2, 7], [4, 7, 9]] + [[9]] * 61  # 64 coalitions: bit 63 set
+    rows, w, member, tot = union_batch(subs, {2: 10, 4: 20, 7: 30, 9: 40}, CPU)
+    assert rows.tolist() == [4, 2, 7, 9] and w.tolist() == [20, 10, 30, 40]
+    m = [int(x) & (2**64 - 1) for x in member.tolist()]
+    assert m[0] == 0b101 and m[1] == 0b011 and m[2] == 0b110
+    assert m[3] == (1 << 2) | sum(1 << s for s in range(3, 64))
+    assert tot.tolist()[:3] == [30.0, 40.0, 90.0]
+
+
+def test_subset_models_union_path_matches_reference_order(doubles):
+    """Store-level: the union path gives each coalition in its own order."""
+    from distributed_learning_simulator_amd.aggregation import ClientUpdateStore
+    from distributed_learning_simulator_amd.layout import ParameterLayout
+    lay = ParameterLayout([("w", (5, 7)), ("b", (3,))])
+    st = ClientUpdateStore(lay, CPU, capacity=6)
+    g = torch.Generator().manual_seed(0)
+    rows = [st.acquire() for _ in range(6)]
+    for r in rows:
+        st.write(r, {"w": torch.randn(5, 7, generator=g), "b": torch.randn(3, generator=g)})
+    n = {r: 100 + 37 * r for r in rows}
+    subs = [[rows[5], rows[0]], [rows[0], rows[3], rows[1]], [rows[2]]]
+    out = st.subset_models(subs, n)
+    U = st.U.numpy()
+    for s, sub in enumerate(subs):
+        assert same_bits(out[s].numpy(), _c.fedavg_ref(U, [n.get(i, 1) for i in range(6)], sub))
+
+
+@pytest.mark.parametrize("tag", ["gtg_50_4", "multiround_12"])
+def test_shapley_host_logic_config5_scale(doubles, tag, tmp_path):
+    """Host logic at config 5's client count (GTG N=50, multiround N=12) with the
+    kernel doubles: SV within 1e-12, same coalitions, metric_1 pickle bytes."""
+    from distributed_learning_simulator_amd.servers.GTG_shapley_value_server import \
+        GTGShapleyValueServer
+    from distributed_learning_simulator_amd.servers.multiround_shapley_value_server import \
+        MultiRoundShapleyValueServer
+    case = next(c for c in G.shapley_large_cases() if c["tag"] == tag)
+    layout = [(nm, tuple(s)) for nm, s in case["layout"]]
+    K = case["K"]
+    target = case["target"]
+    gtg = tag.startswith("gtg")
+    cls = GTGShapleyValueServer if gtg else MultiRoundShapleyValueServer
+    kw = {} if gtg else {"metric_dir": str(tmp_path)}
+    server = cls(tester=None, worker_number=K, synchronous=True, device=CPU, **kw)
+    server._set_prev_model(G.split(torch.tensor(case["prev"]), layout))
+
+    def util(model, metric_type="acc"):
+        v = np.concatenate([np.asarray(model[nm], np.float64).reshape(-1) for nm, _ in layout])
+        d = v - target
+        return float(1.0 / (1.0 + float(np.dot(d, d)) / case["scale"]))
+
+    server.get_metric = util
+    np.random.seed(case["seed"])
+    for i in range(K):
+        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(case["U"][i], layout).items()}
+        server.worker_data_queue.add_task((i, int(case["n"][i]), d))
+    sv = server.shapley_values[1]
+    for kk, v in case["sv"].items():
+        assert abs(float(sv[int(kk)]) - v) <= 1e-12, kk
+    assert {tuple(s) for s in server.evaluated_subsets} == set(case["evaluated"])
+    if not gtg:
+        assert (tmp_path / "metric_1").read_bytes() == case["metric_pickle"]

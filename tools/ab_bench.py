@@ -131,6 +131,34 @@ def setup(dev, want=()):
                                                          st.sz.stride(0) // 2, ptr(rows0), ptr(w),
                                                          100, tot, ptr(qo), stream()),
                           100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+    # Shapley default path: 50 coalitions (members with p = 1/2) over 50 clients,
+    # each client row read once per batch (dls_subset_fedavg_union_f32)
+    from distributed_learning_simulator_amd.aggregation import union_batch
+    gc = torch.Generator().manual_seed(5)
+    member = torch.rand((50, 50), generator=gc) < 0.5
+    member[:, 0] = True
+    subs = [[k for k in range(50) if member[s, k]] for s in range(50)]
+    nrow = {k: int(w[k]) for k in range(50)}
+    ur, uwt, um, ut = union_batch(subs, nrow, dev)
+    uo = torch.empty((50, P), device=dev)
+    pairs = int(member.sum())
+    W["union"] = (lambda L: L.dls_subset_fedavg_union_f32(ptr(U), P, ptr(ur), ptr(uwt), ptr(um), 50,
+                                                          ptr(ut), 50, P, ptr(uo), P, stream()),
+                  100 * P * 4)
+    off, fr, fw, ft = [0], [], [], []
+    for sub in subs:
+        fr += sub
+        fw += [nrow[k] for k in sub]
+        ft.append(float(sum(nrow[k] for k in sub)))
+        off.append(len(fr))
+    t_off = torch.tensor(off, dtype=torch.int32, device=dev)
+    t_fr = torch.tensor(fr, dtype=torch.int32, device=dev)
+    t_fw = torch.tensor(fw, dtype=torch.float32, device=dev)
+    t_ft = torch.tensor(ft, dtype=torch.float32, device=dev)
+    W["subset_exact"] = (lambda L: L.dls_subset_fedavg_f32(ptr(U), P, ptr(t_off), ptr(t_fr),
+                                                           ptr(t_fw), ptr(t_ft), 50, P, ptr(uo), P,
+                                                           stream()), 100 * P * 4)
+    print("union member pairs", pairs, flush=True)
     C = torch.rand((50, 50), generator=g, device=dev)
     C = C / C.sum(1, keepdim=True)
     go = torch.empty((50, P), device=dev)
