@@ -42,6 +42,10 @@ from distributed_learning_simulator_amd.model_shapes import resnet18_cifar, vgg1
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
+# f32 VALU issue roof: 256 CUs x 4 SIMDs x 32 lanes per clock x 2.4 GHz = 78.6 T
+# lane-ops/s (a v_pk_* op = 2 lane-ops per lane; MI355X_MICROARCH.md: the f32
+# VALU peak is 64 FLOP/clk/SIMD with FMAs counted twice)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 SEED = 20250127
 
 
@@ -86,11 +90,15 @@ def roofline(kernel, bytes_per_launch, kernel_ms, bound="hbm", flops_per_launch=
     if bound == "hbm":
         achieved = bytes_per_launch / avg_s / 1e9
         peak, unit = HBM_PEAK_GBS, "GB/s"
+    elif bound == "valu":  # flops_per_launch = f32 VALU lane-ops at the minimum op count
+        achieved = flops_per_launch / avg_s / 1e12
+        peak, unit = VALU_PEAK_TOPS, "T lane-op/s"
     else:
         achieved = flops_per_launch / avg_s / 1e12
         peak, unit = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
-    return {"kernel": kernel, "bound": bound, "achieved": round(achieved, 2), "peak": peak,
-            "unit": unit, "frac": round(achieved / peak, 4), "traffic": load_traffic(key or kernel),
+    return {"kernel": kernel, "bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": unit, "frac": round(achieved / peak, 4),
+            "traffic": load_traffic(key) if key else None,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "avg_launch_us": round(avg_s * 1e6, 2)}
 
@@ -110,9 +118,12 @@ def synth_updates(K, P, dev, seed):
 
 
 # ----------------------------------------------------------------- FedAvg
-def bench_fedavg(args, dev, rank, world):
+def bench_fedavg(args, dev, rank, world, scaling="weak"):
+    """Config 2.  weak: args.clients clients per GPU; strong: args.clients clients in
+    total, dealt round-robin over the ranks (worker_id % world, simulator.py:68)."""
     layout = ParameterLayout(resnet18_cifar())
-    P, K = layout.P, args.clients
+    P = layout.P
+    K = args.clients if scaling == "weak" else len(range(rank, args.clients, world))
     U, n = synth_updates(K, P, dev, SEED + 1 + rank)
     # global sample count (FedAvg over all ranks' clients)
     n_all = torch.tensor([sum(n)], dtype=torch.float64, device=dev)
@@ -148,13 +159,16 @@ def bench_fedavg(args, dev, rank, world):
     wall = float(t.item())
     ms = wall / args.steps * 1e3
     upd_bytes = layout.numel * 4  # one client update (fp32, unpadded)
-    value = world * K * upd_bytes / (ms / 1e3) / 1e9
+    total_clients = world * K if scaling == "weak" else args.clients
+    value = total_clients * upd_bytes / (ms / 1e3) / 1e9
     bytes_per_launch = K * P * 4 + P * 4
-    rf = roofline("dls_fedavg_f32", bytes_per_launch, kms, key="headline")
+    rf = roofline("dls_fedavg_f32", bytes_per_launch, kms,
+                  key="headline" if scaling == "weak" and world == 1 else None)
     if world > 1:  # the events bracket all chunks' kernels (and interleaved RCCL enqueue)
         rf["note"] = "launch window includes chunked all-reduce overlap"
     del U
-    return value, ms, rf, {"clients_per_gpu": K, "params": layout.numel, "padded_row": P}
+    return value, ms, rf, {"clients_per_gpu": K, "clients_total": total_clients,
+                           "params": layout.numel, "padded_row": P}
 
 
 # ------------------------------------------------------------ components
@@ -229,11 +243,12 @@ def bench_sign(args, dev):
     }
 
 
-def _quant_store(dev, K, seed):
-    """K synthetic VGG-16 int8 payloads (per-channel symmetric) in a device store."""
+def _quant_store(dev, K, seed, shapes=None):
+    """K synthetic int8 payloads (per-channel symmetric weights, fp32 1-d tensors) of
+    the given model (default VGG-16) in a device store."""
     from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
     template = {}
-    for name, s in vgg16():
+    for name, s in (shapes or vgg16()):
         if len(s) >= 2:
             template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
                               torch.zeros(s[0], dtype=torch.int64))
@@ -325,9 +340,8 @@ def bench_quant_sharded(args, dev, world, rank):
             "dequant_kernel_us": round(sum(kms) / len(kms) * 1e3, 2)}
 
 
-def bench_quant(args, dev):
-    store, n, client_bytes, p_logical = _quant_store(dev, 100, SEED + 4)
-    K = len(n)
+def bench_quant(args, dev, K=100, shapes=None, model="VGG-16", key="fed_quant"):
+    store, n, client_bytes, p_logical = _quant_store(dev, K, SEED + 4, shapes)
     out = torch.empty(store.layout.P, device=dev)
     rows_t = torch.arange(K, dtype=torch.int32, device=dev)
     w_t = torch.tensor(n, dtype=torch.float32, device=dev)
@@ -341,17 +355,98 @@ def bench_quant(args, dev):
         if b is not None:
             b.record()
 
-    wall, kms = timed_launches(step, args.steps, args.warmup)
-    ms = wall / args.steps * 1e3
+    steps = args.steps if K <= 100 else max(3, args.steps // 4)
+    wall, kms = timed_launches(step, steps, min(args.warmup, 3))
+    ms = wall / steps * 1e3
     bytes_per_launch = K * client_bytes + 4 * store.layout.numel
+    # VALU roof at the reference's minimum op count: per int8 element and client
+    # cvt + fl(q - zp)*s + *n_i + /N (two-constant: 2 ops, Markstein: 3) + add
+    from distributed_learning_simulator_amd._native import two_constant_division
+    div_ops = 2 if two_constant_division(total) else 3
+    valu_ops = K * p_logical * (4 + div_ops)
     del store
     return {
-        "config": "fed_quant 8-bit, 100 clients x VGG-16, fused dequant + FedAvg (bit-exact)",
+        "config": f"fed_quant 8-bit, {K} clients x {model}, fused dequant + FedAvg (bit-exact)",
         "value": round(K * client_bytes / (ms / 1e3) / 1e9, 2),
         "unit": "GB/s (int8 client updates)",
         "fp32_logical_GBps": round(K * p_logical * 4 / (ms / 1e3) / 1e9, 2),
         "ms_per_step": round(ms, 4),
-        "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms, key="fed_quant"),
+        "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms, key=key),
+        "valu_roof": roofline("dls_dequant_fedavg", bytes_per_launch, kms, bound="valu",
+                              flops_per_launch=valu_ops),
+    }
+
+
+def bench_quant_k1000(args, dev):
+    """North-star: quantized aggregation of 1000 ResNet-18-sized int8 updates."""
+    return bench_quant(args, dev, K=1000, shapes=resnet18_cifar(), model="ResNet-18",
+                       key="fed_quant_k1000")
+
+
+def _shapley_coalitions(K, S, seed):
+    """S coalitions of K clients, members with probability 1/2 (client 0 always),
+    as sorted tuples (how the Shapley servers pass them)."""
+    g = torch.Generator().manual_seed(seed)
+    member = torch.rand((S, K), generator=g) < 0.5
+    member[:, 0] = True
+    return [tuple(k for k in range(K) if member[s, k]) for s in range(S)]
+
+
+def bench_shapley_exact(args, dev):
+    """Config 5a, the Shapley servers' default path: S bit-exact subset models of K
+    clients in one dls_subset_fedavg_union_f32 launch (each client row read once)."""
+    from distributed_learning_simulator_amd.aggregation import union_batch
+    layout = ParameterLayout(resnet18_cifar())
+    P, K, S = layout.P, 50, args.subsets
+    U, n = synth_updates(K, P, dev, SEED + 5)
+    subs = _shapley_coalitions(K, S, SEED + 5)
+    t = union_batch([list(c) for c in subs], dict(enumerate(n)), dev)
+    out = torch.empty((S, P), device=dev)
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.subset_fedavg_union(U, *t, P, out)
+        if b is not None:
+            b.record()
+
+    wall, kms = timed_launches(step, args.steps, args.warmup)
+    ms = wall / args.steps * 1e3
+    pairs = sum(len(c) for c in subs)
+    waves = -(-S // 8)
+    # minimum VALU lane-ops: per parameter, 4 per (client, coalition) membership
+    # (Markstein q0, r, q + the add) and 4/4 per (client, wave) for t = x * n_i
+    valu_ops = layout.numel * (4 * pairs + K * waves)
+    bytes_per_launch = (K + S) * P * 4
+    # the per-coalition kernel on the same batch, for comparison
+    off, fr, fw, ft = [0], [], [], []
+    for c in subs:
+        fr += c
+        fw += [n[k] for k in c]
+        ft.append(float(sum(n[k] for k in c)))
+        off.append(len(fr))
+    tt = [torch.tensor(v, dtype=dt, device=dev) for v, dt in
+          ((off, torch.int32), (fr, torch.int32), (fw, torch.float32), (ft, torch.float32))]
+
+    def step_pc(a=None, b=None):
+        if a is not None:
+            a.record()
+        _native.subset_fedavg(U, *tt, P, out)
+        if b is not None:
+            b.record()
+
+    _, kms_pc = timed_launches(step_pc, max(3, args.steps // 4), 1)
+    del U, out
+    return {
+        "config": f"Shapley subset models, default bit-exact path: {S} coalitions (members p=1/2, "
+                  f"{pairs} memberships) of 50 clients x ResNet-18, one union launch",
+        "value": round(S / (ms / 1e3), 1), "unit": "subset models/s",
+        "ms_per_step": round(ms, 4),
+        "roofline": roofline("dls_subset_fedavg_union_f32", bytes_per_launch, kms,
+                             key="shapley_exact"),
+        "valu_roof": roofline("dls_subset_fedavg_union_f32", bytes_per_launch, kms, bound="valu",
+                              flops_per_launch=valu_ops),
+        "per_coalition_kernel_ms": round(sum(kms_pc) / len(kms_pc), 4),
     }
 
 
@@ -390,67 +485,54 @@ def bench_shapley_gemm(args, dev):
     }
 
 
-def bench_shapley_evals(args, dev):
-    """Config 5b: Shapley utility evaluations — subset model (reference-order
-    kernel) + CIFAR-10-shaped test-set inference of ResNet-18 (fp32)."""
-    from distributed_learning_simulator_amd.layout import ParameterLayout as PL
+def _shapley_eval_server(args, dev, K=50):
+    """A Shapley server (the servers' own evaluate_subsets path) with a ResNet-18
+    tester on a CIFAR-10-shaped synthetic test set labelled by a fixed teacher, and
+    K clients = teacher + client noise (so utilities differ)."""
     from distributed_learning_simulator_amd.model_util import ModelUtil
     from distributed_learning_simulator_amd.models import ResNet18
+    from distributed_learning_simulator_amd.servers.shapley_value_server import ShapleyValueServer
+    from distributed_learning_simulator_amd.trainer import Inferencer
     torch.manual_seed(SEED + 6)
     teacher = ResNet18().to(dev).eval()
     X = torch.randn(args.eval_images, 3, 32, 32, device=dev)
     with torch.no_grad():
         y = torch.cat([teacher(X[i:i + 1000]).argmax(1) for i in range(0, X.shape[0], 1000)])
+    tester = Inferencer(ResNet18().to(dev), (X, y), batch_size=1000, device=dev)
+    server = ShapleyValueServer(tester=tester, worker_number=K, synchronous=True, device=dev)
     base = ModelUtil(teacher).get_parameter_dict()
-    layout = PL.from_dict(base)
-    K = 50
-    row = layout.flatten(base, device=dev)
-    U = row[None, :].repeat(K, 1)
-    U.add_(torch.randn_like(U) * 0.002)
-    n = [100 + 17 * i for i in range(K)]
-    g = torch.Generator().manual_seed(SEED + 6)
-    coalitions = [sorted(torch.randperm(K, generator=g)[: 1 + i % K].tolist())
-                  for i in range(args.evals + 2)]
-    model = ResNet18().to(dev).eval().to(memory_format=torch.channels_last)
-    X = X.contiguous(memory_format=torch.channels_last)  # NHWC convs (tools/eval_probe.py)
-    mu = ModelUtil(model)
-    autocast = {"enabled": False}
+    g = torch.Generator(device=dev).manual_seed(SEED + 6)
+    for wid in range(K):
+        d = {k: v + torch.randn(v.shape, generator=g, device=dev) * 0.002 for k, v in base.items()}
+        server.parameters[wid] = (100 + 17 * wid, d)
+    return server
 
-    def one_eval(c):
-        rows = torch.tensor(c, dtype=torch.int32, device=dev)
-        w = torch.tensor([n[i] for i in c], dtype=torch.float32, device=dev)
-        out = torch.empty(layout.P, device=dev)
-        _native.fedavg(U, rows, w, float(sum(n[i] for i in c)), layout.P, out)
-        mu.load_parameter_dict(layout.views(out))
-        correct = 0
-        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16,
-                                             enabled=autocast["enabled"]):
-            for i in range(0, X.shape[0], 1000):
-                correct += (model(X[i:i + 1000]).argmax(1) == y[i:i + 1000]).sum()
-        correct = int(correct)
-        return correct / X.shape[0]
 
-    def timed():
-        for c in coalitions[:2]:
-            one_eval(c)  # MIOpen kernel selection
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        accs = [one_eval(c) for c in coalitions[2:]]
-        torch.cuda.synchronize()
-        return accs, time.perf_counter() - t0
-
-    accs, el = timed()
-    autocast["enabled"] = True
-    accs16, el16 = timed()
-    del U
-    return {"config": f"Shapley utility evals: subset model + ResNet-18 inference on "
-                      f"{args.eval_images} CIFAR-10-shaped images (fp32, NHWC, batch 1000), "
-                      f"50 clients",
-            "value": round(len(accs) / el, 3), "unit": "subset-evals/s per GPU",
-            "ms_per_eval": round(el / len(accs) * 1e3, 2),
-            "utility_range": [round(min(accs), 4), round(max(accs), 4)],
-            "bf16_autocast_value": round(len(accs16) / el16, 3),
-            "bf16_max_utility_diff": round(max(abs(a - b) for a, b in zip(accs, accs16)), 4)}
+def bench_shapley_evals(args, dev, world=1, rank=0):
+    """Config 5b: Shapley utility evaluations through ShapleyValueServer.evaluate_subsets
+    (batched bit-exact subset models + ResNet-18 test-set inference; on N ranks the
+    coalitions are dealt round-robin and the utilities all-reduced).  Weak scaling:
+    args.evals coalitions per GPU."""
+    server = _shapley_eval_server(args, dev)
+    coal = _shapley_coalitions(50, (args.evals + 2) * world, SEED + 7)
+    server.evaluate_subsets(coal[: 2 * world])  # MIOpen kernel selection, warm caches
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    vals = server.evaluate_subsets(coal[2 * world:])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        el = _max_over_ranks(el, dev)
+    n = len(coal) - 2 * world
+    del server
+    return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
+                      f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
+                      f"{args.eval_images} CIFAR-10-shaped images (fp32, NHWC, batch 1000)",
+            "value": round(n / el, 3), "unit": "subset-evals/s (all GPUs)",
+            "ms_per_eval_per_gpu": round(el / n * world * 1e3, 2),
+            "utility_range": [round(min(vals), 4), round(max(vals), 4)]}
 
 
 # ---------------------------------------------------------- CPU baseline
@@ -475,6 +557,8 @@ def cpu_baseline(args):
             break
     per = el / reps
     P = sum(math.prod(s) for _, s in shapes)
+    shapley = cpu_shapley_eval(args, clients, n, threads)
+    del clients
     model = ""
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -487,7 +571,40 @@ def cpu_baseline(args):
             "sample": f"{Kc} ResNet-18 client dicts (fp32, 62 tensors), reference torch op "
                       f"sequence, {reps} reps in {el:.1f}s",
             "cpu_model": model or platform.processor(), "ms_per_aggregation": round(per * 1e3, 2),
-            "components": cpu_components(args, threads)}
+            "components": {"shapley_evals": shapley, **cpu_components(args, threads)}}
+
+
+def cpu_shapley_eval(args, clients, n, threads):
+    """Config 5b on the host: one Shapley utility evaluation the reference's way —
+    get_subset_model's torch op sequence over a 25-client coalition
+    (servers/fed_server.py:52-65) + ResNet-18 inference on the test set
+    (servers/fed_server.py:26-32) — timed on a bounded image sample and scaled to
+    the full test set (inference time is linear in the image count)."""
+    from oracle.fedavg import fedavg_torch_cpu  # test infrastructure, timed only
+    from distributed_learning_simulator_amd.models import ResNet18
+    coal = list(range(0, len(clients), 2))[:25]
+    t0 = time.perf_counter()
+    model = fedavg_torch_cpu(clients, n, coal)
+    t_subset = time.perf_counter() - t0
+    net = ResNet18().eval()
+    with torch.no_grad():
+        for k, p in net.named_parameters():
+            p.copy_(model[k])
+    g = torch.Generator().manual_seed(SEED + 11)
+    imgs = args.cpu_eval_images
+    X = torch.randn(imgs, 3, 32, 32, generator=g)
+    with torch.no_grad():
+        net(X[:100])  # warm
+        t0 = time.perf_counter()
+        for i in range(0, imgs, 250):
+            net(X[i:i + 250]).argmax(1)
+        t_inf = (time.perf_counter() - t0) * args.eval_images / imgs
+    per_eval = t_subset + t_inf
+    return {"value": round(1.0 / per_eval, 4), "unit": "subset-evals/s", "cores": threads,
+            "kind": "port",
+            "sample": f"25-client ResNet-18 subset model (reference torch op sequence) + "
+                      f"inference on {imgs} images, scaled to {args.eval_images}",
+            "s_per_eval": round(per_eval, 2), "s_subset_model": round(t_subset, 3)}
 
 
 def cpu_components(args, threads):
@@ -544,19 +661,24 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--clients", type=int, default=100, help="client updates per GPU")
+    ap.add_argument("--clients", type=int, default=100,
+                    help="config-2 client updates: per GPU (weak) or in total (strong)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="the headline's scaling; at N > 1 the other one is a component")
     ap.add_argument("--chunks", type=int, default=3, help="all-reduce pipeline chunks (N>1)")
     ap.add_argument("--subsets", type=int, default=50)
-    ap.add_argument("--evals", type=int, default=8, help="timed Shapley utility evaluations")
+    ap.add_argument("--evals", type=int, default=8, help="timed Shapley utility evaluations per GPU")
     ap.add_argument("--eval-images", type=int, default=10000)
     ap.add_argument("--quick", action="store_true", help="headline only (no components)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
-    ap.add_argument("--only", default="", help="comma list: headline,fedavg_k1000,sign_vote,"
-                    "sign_vote_sharded,fed_quant_sharded,"
-                                                "fed_quant,shapley_gemm,shapley_evals")
-    ap.add_argument("--cpu-clients", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma list: headline,fedavg_other_scaling,"
+                    "fedavg_k1000,sign_vote,fed_quant,fed_quant_k1000,shapley_exact,shapley_gemm,"
+                    "shapley_evals,sign_vote_sharded,fed_quant_sharded")
+    ap.add_argument("--cpu-clients", type=int, default=100,
+                    help="CPU baseline: clients of the config-2 aggregation (full K = 100)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-eval-images", type=int, default=500)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -573,26 +695,36 @@ def main():
             dist.init_process_group(args.backend)
 
     only = set(args.only.split(",")) if args.only else None
+    want = lambda name: only is None or name in only  # noqa: E731
     value = ms = rf = None
     extra = {}
-    if only is None or "headline" in only:
-        value, ms, rf, extra = bench_fedavg(args, dev, rank, world)
+    if want("headline"):
+        value, ms, rf, extra = bench_fedavg(args, dev, rank, world, args.scaling)
     components = {}
-    if world > 1 and not args.quick:  # the sharded servers' rounds: every rank takes part
-        for name, fn in (("sign_vote_sharded", bench_sign_sharded),
-                         ("fed_quant_sharded", bench_quant_sharded)):
-            if only is not None and name not in only:
+    if world > 1 and not args.quick:  # collectives: every rank takes part, no per-rank skipping
+        other = "strong" if args.scaling == "weak" else "weak"
+        coll = [("fedavg_other_scaling",
+                 lambda *a: dict(zip(("value", "ms_per_step", "roofline", "config"),
+                                     bench_fedavg(args, dev, rank, world, other)),
+                                 scaling=other, unit="GB/s")),
+                ("sign_vote_sharded", lambda *a: bench_sign_sharded(args, dev, world, rank)),
+                ("fed_quant_sharded", lambda *a: bench_quant_sharded(args, dev, world, rank)),
+                ("shapley_evals", lambda *a: bench_shapley_evals(args, dev, world, rank))]
+        for name, fn in coll:
+            if not want(name):
                 continue
-            components[name] = fn(args, dev, world, rank)  # collective: no per-rank skipping
+            components[name] = fn()
             if rank == 0:
                 log(name, json.dumps(components[name]))
             torch.cuda.empty_cache()
     if not args.quick and rank == 0:
-        for name, fn in (("fedavg_k1000", bench_fedavg_k1000), ("sign_vote", bench_sign),
-                         ("fed_quant", bench_quant),
-                         ("shapley_gemm", bench_shapley_gemm),
-                         ("shapley_evals", bench_shapley_evals)):
-            if only is not None and name not in only:
+        local_parts = [("fedavg_k1000", bench_fedavg_k1000), ("sign_vote", bench_sign),
+                       ("fed_quant", bench_quant), ("fed_quant_k1000", bench_quant_k1000),
+                       ("shapley_exact", bench_shapley_exact), ("shapley_gemm", bench_shapley_gemm)]
+        if world == 1:
+            local_parts.append(("shapley_evals", bench_shapley_evals))
+        for name, fn in local_parts:
+            if not want(name):
                 continue
             try:
                 components[name] = fn(args, dev)
@@ -606,6 +738,7 @@ def main():
     if world > 1:
         dist.barrier()
     if rank == 0:
+        total_clients = extra.get("clients_total", args.clients)
         line = {
             # BASELINE.json's metric; `value` is its first part (client-update GB/s),
             # the second part (Shapley subset-evals/s) is `shapley_subset_evals_per_s`
@@ -614,9 +747,11 @@ def main():
             "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4) if ms is not None else None,
             "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": "FedAvg aggregation of 100 synthetic ResNet-18 (11.2M-param "
-                                   "fp32) client updates per GPU, bit-exact reference order",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"FedAvg aggregation of {total_clients} synthetic ResNet-18 "
+                                   f"(11.2M-param fp32) client updates "
+                                   f"({'per GPU' if args.scaling == 'weak' else 'in total'}), "
+                                   "bit-exact reference order",
                        "parallelism": f"clients sharded over {world} GPU(s) + RCCL all-reduce",
                        **extra},
             "roofline": rf, "cpu_baseline": cpu,

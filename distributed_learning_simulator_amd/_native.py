@@ -116,6 +116,12 @@ def _stream(stream=None, like=None):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
+def two_constant_division(divisor):
+    """1 if the dequant kernels divide by fl32(divisor) with the two-constant method
+    (proven correctly rounded for it by the library's exhaustive host check)."""
+    return int(lib().dls_two_constant_division(float(divisor)))
+
+
 def require_gpu():
     if not torch.cuda.is_available():
         raise RuntimeError("distributed_learning_simulator_amd needs a ROCm GPU (no CPU fallback)")

@@ -216,159 +216,216 @@ __global__ __launch_bounds__(kBlock) void k_subset_exact(const f32x4 *__restrict
 // every coalition's members in that coalition's own order (the host orders the
 // union so; sorted worker-id tuples always are).  So each client row is read
 // from HBM once per batch instead of once per coalition containing it:
-//   for client j of the union:  t = fl(x * fl32(n_j))
-//       for every coalition s holding j (bit s of member[j]):  acc_s = fl(acc_s + fl(t / N_s))
+//   t_j = fl(x_j * fl32(n_j)) once per client;
+//   acc_s = fl(acc_s + fl(t_j / N_s)) for the members j of coalition s, in union order
 // which is term for term the op sequence of servers/fed_server.py:57-65 for
 // each coalition (acc_s starts at -0: -0 + q == q, "the first client is assigned").
 //
-// Block = one tile of 256 parameters (a lane owns 4), one wave per <= kSubsetSB
-// coalitions (spread evenly): the waves of a block load the same 1 KiB of each client row at the
-// same time (one HBM read, the others served by the CU's L1 / the XCD's L2) and
-// each keeps its kSubsetSB accumulators in registers.  Membership is a
-// wave-uniform bit test (SALU branch), so a coalition that does not hold client
-// j costs nothing.  Algorithmic bytes: (Ku + S) * 4 per parameter; VALU: 4 per
-// parameter per (client, coalition) membership (multiply-add Markstein division +
-// add) + 4 per parameter per (client, wave) for t.  At S = Ku = 50 with
-// coalitions half full the VALU issue, not HBM, is the roof.
-#ifndef DLS_SUBSET_SB
-#define DLS_SUBSET_SB 8  // coalitions per wave: 10 VGPRs each (SB 8 -> 135 VGPRs, 3 waves / SIMD)
-#endif
-#ifndef DLS_SUBSET_UB
-#define DLS_SUBSET_UB 4  // clients per double-buffered batch
-#endif
-constexpr int kSubsetSB = DLS_SUBSET_SB;
-constexpr int kSubsetUB = DLS_SUBSET_UB;
-constexpr int kSubsetMaxBlock = 64 * ((DLS_SUBSET_UNION_MAX + kSubsetSB - 1) / kSubsetSB);
+// Persistent blocks of kUnionWaves waves walk 256-parameter tiles (a lane owns 4
+// parameters).  Per tile the waves stage t_j of the <= 64 clients in LDS (each
+// wave a few clients, register-staged: the NEXT tile's rows are loaded while
+// this tile is computed, so HBM latency hides behind a whole tile of work);
+// then wave w computes its coalitions (w, w + W, ...) coalition-major: it walks
+// the coalition's member list (built once per block in LDS from the member
+// masks) with 4 independent Markstein quotients in flight and the adds in list
+// order.  No per-membership branches; a wave's results are stored at the start
+// of the next tile, just before that tile's loads are issued, so the loads never
+// wait behind younger stores (vmcnt counts both, in order).
+// Algorithmic bytes: (Ku + S) * 4 per parameter.  VALU per parameter: 4 per
+// (client, coalition) membership (Markstein's 3 + the add) + 1 per client for t;
+// at S = Ku = 50 with half-full coalitions the VALU issue, not HBM, is the roof
+// (DESIGN.md §4).
+constexpr int kUnionChunk = 64;  // clients per launch (the host splits larger unions)
 
-template <int SB, int UB>
-__global__ __launch_bounds__(kSubsetMaxBlock) void k_subset_union(const f32x4 *__restrict__ Uv, int64_t ldu4,
-                                                      const int32_t *__restrict__ urows,
-                                                      const float *__restrict__ uw,
-                                                      const uint64_t *__restrict__ member, int Ku,
-                                                      const float *__restrict__ sub_total, int S,
-                                                      int64_t P4, f32x4 *__restrict__ out,
-                                                      int64_t ldo4) {
+// in_fast_range (dls_common.h) of all four: 2^-60 <= |t| < 2^61 on the bit
+// patterns (min / max of |bits|: zeros, denormals, inf and nan all fail)
+__device__ __forceinline__ bool all_in_fast_range(f32x4 t) {
+    const uint32_t a = __float_as_uint(t.x) & 0x7fffffffu, b = __float_as_uint(t.y) & 0x7fffffffu;
+    const uint32_t c = __float_as_uint(t.z) & 0x7fffffffu, d = __float_as_uint(t.w) & 0x7fffffffu;
+    const uint32_t mn = min(min(a, b), min(c, d)), mx = max(max(a, b), max(c, d));
+    return mn >= (67u << 23) && mx < (188u << 23);
+}
+constexpr int kUnionWaves = 8;   // waves per block: <= 8 clients staged, <= KW coalitions each
+
+// KW = ceil(S / 8) coalitions per wave (a template parameter, so that every wave
+// issues exactly KW stores and NL loads per tile: the compiler's vmcnt waits
+// are then exact, and waiting for the next tile's loads never waits for this
+// tile's younger stores).
+template <int KW, bool ACC>
+__global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
+    const f32x4 *__restrict__ Uv, int64_t ldu4, const int32_t *__restrict__ urows,
+    const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku,
+    const float *__restrict__ sub_total, int S, int64_t P4, int64_t ntiles,
+    f32x4 *__restrict__ out, int64_t ldo4) {
+    constexpr int W = kUnionWaves, NL = kUnionChunk / kUnionWaves;
+    // 69 KiB in all, so two blocks (16 waves) share a CU
+    __shared__ f32x4 ts[kUnionChunk * 64];                    // 64 KiB: t_j of this tile
+    __shared__ uint8_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk];  // member positions, per coalition
+    __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];               // {y, y, N, N} per coalition
+    __shared__ uint32_t tbad[W];                              // per loader wave: t out of range
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;  // block-uniform
     const int lane = __lane_id();
-    // the S coalitions are spread evenly over the block's waves (<= SB each)
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nwv = blockDim.x >> 6;
-    const int s0 = wv * S / nwv;
-    const int ns = (wv + 1) * S / nwv - s0;  // wave-uniform, 1..SB by the launch geometry
-    const int64_t i0 = (int64_t)blockIdx.x * 64 + lane;
-    const int64_t iq = i0 < P4 ? i0 : P4 - 1;  // every lane stays: the tables need all 64
-    // per-coalition divisor N_s and y_s = RN(1/N_s) (wave-uniform values, kept in
-    // VGPRs: 2*SB SGPRs beside the client tables would spill)
-    float bs[SB];
-    f32x2 ys[SB];  // {y, y}: the packed multiply-adds take it as a register pair
-    int allfast = 1;
+    // client table: lane j holds client j's row and weight
+    const int kk = min(lane, Ku - 1);
+    const int tr = urows[kk];
+    const float tw = uw[kk];
+    const uint64_t mj = lane < Ku ? member[kk] : 0ull;
+    // this wave's coalitions: wv + W k (k < nk); a wave without one (S < 8)
+    // recomputes coalition S - 1 (the same bits, stored twice)
+    int nk = (S - wv + W - 1) / W;
+    const int cdup = nk > 0 ? -1 : S - 1;
+    nk = nk > 0 ? nk : 1;
+    auto coal = [&](int k) { return cdup >= 0 ? cdup : wv + W * k; };
+    int len[KW];
+    int fast = (int)(__ballot(!(tw >= 1.0f && tw <= 16777216.0f)) == 0);  // 1 <= n_j <= 2^24
 #pragma unroll
-    for (int s = 0; s < SB; ++s) {
-        bs[s] = s < ns ? sub_total[s0 + s] : 1.f;
-        const float y = (float)(1.0 / (double)bs[s]);
-        ys[s] = f32x2{y, y};
-        allfast &= (int)(bs[s] >= 1.0f && bs[s] <= 2147483648.0f);
-    }
-    f32x4 acc[SB];
-#pragma unroll
-    for (int s = 0; s < SB; ++s) acc[s] = f32x4{-0.f, -0.f, -0.f, -0.f};
-    const uint32_t smask = (uint32_t)((1ull << ns) - 1ull);
-    // client table: lane l holds client (chunk base + l); the next chunk is in flight
-    auto fetch = [&](int k, int &r, float &w, uint32_t &m) {
-        const int kk = min(k + lane, Ku - 1);
-        r = urows[kk];
-        w = uw[kk];
-        m = k + lane < Ku ? (uint32_t)(member[kk] >> s0) & smask : 0u;  // past the end: no work
-    };
-    int nr;
-    float nw;
-    uint32_t nm;
-    fetch(0, nr, nw, nm);
-    // Common case only: every t of the wave in Markstein's range and every
-    // divisor in [1, 2^31].  Otherwise (zeros, denormals, huge values, inf / nan)
-    // the wave flags `redo` and recomputes its tile after the loop on a slow,
-    // compact path, so the hot loop carries no fix-up code or registers.
-    int redo = !allfast;
-    auto one = [&](f32x4 x, float wk, uint32_t m) {
-        f32x4 t;
-        t.x = x.x * wk;
-        t.y = x.y * wk;
-        t.z = x.z * wk;
-        t.w = x.w * wk;
-        const int ok = (int)in_fast_range(t.x) & (int)in_fast_range(t.y) &
-                       (int)in_fast_range(t.z) & (int)in_fast_range(t.w);
-        redo |= (int)(__ballot(!ok) != 0);
-#pragma unroll
-        for (int s = 0; s < SB; ++s) {
-            if (m & (1u << s)) {  // wave-uniform: a scalar branch
-                // Markstein on element pairs (v_pk_mul / v_pk_fma: the scalar ops' roundings)
-                const f32x2 b2 = f32x2{bs[s], bs[s]};
-                const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
-                const f32x2 ql0 = tl * ys[s], qh0 = th * ys[s];
-                const f32x2 ql = __builtin_elementwise_fma(
-                    __builtin_elementwise_fma(-ql0, b2, tl), ys[s], ql0);
-                const f32x2 qh = __builtin_elementwise_fma(
-                    __builtin_elementwise_fma(-qh0, b2, th), ys[s], qh0);
-                acc[s] = add4(acc[s], f32x4{ql.x, ql.y, qh.x, qh.y});
+    for (int k = 0; k < KW; ++k) {
+        len[k] = 0;
+        if (k < nk) {
+            const int c = coal(k);
+            const uint64_t in = __ballot((mj >> c) & 1ull);
+            len[k] = __popcll(in);
+            if (cdup < 0) {  // one wave builds each coalition's tables
+                if ((mj >> c) & 1ull)
+                    lst[c][__builtin_amdgcn_mbcnt_hi((uint32_t)(in >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)in, 0u))] =
+                        (uint8_t)lane;
+                const float b = sub_total[c];
+                const float y = (float)(1.0 / (double)b);
+                if (lane == 0) cst[c] = f32x4{y, y, b, b};
             }
+            const float b = sub_total[c];
+            fast &= (int)(b >= 1.0f && b <= 2147483648.0f);
+        }
+    }
+    // loader slots: wave wv stages clients wv + W l, l < NL (past Ku: a duplicate
+    // row, loaded but never staged, so the load count is static)
+    f32x4 R[NL];
+    auto issue = [&](int64_t t) {
+        const int64_t i0 = t * 64 + lane;
+        const int64_t iq = i0 < P4 ? i0 : P4 - 1;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+            const int j = min(wv + W * l, Ku - 1);
+            const int64_t r = __builtin_amdgcn_readlane(tr, j);
+            R[l] = load4<false>(Uv + r * ldu4 + iq);
         }
     };
-    for (int base = 0; base < Ku; base += 64) {
-        const int tr = nr;
-        const float tw = nw;
-        const uint32_t tm = nm;
-        fetch(base + 64, nr, nw, nm);
-        // batches of UB clients, double-buffered; past the chunk's end a batch
-        // loads a valid duplicate row with no membership (no work), so every load
-        // is unconditional (exact vmcnt waits) and there is no tail loop
-        const int nb = (min(64, Ku - base) + UB - 1) / UB;
-        auto load = [&](int j0, f32x4 (&x)[UB], float (&wk)[UB], uint32_t (&mk)[UB]) {
+    f32x4 ain[KW];  // ACC: running sums of a previous 64-client chunk
+    auto load_acc = [&](int64_t t) {
+        const int64_t i0 = t * 64 + lane;
+        const int64_t iq = i0 < P4 ? i0 : P4 - 1;
 #pragma unroll
-            for (int u = 0; u < UB; ++u) {
-                const int j = min(j0 + u, 63);
-                const int64_t r = __builtin_amdgcn_readlane(tr, j);
-                wk[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
-                mk[u] = j0 + u < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)tm, j) : 0u;
-                x[u] = load4<false>(Uv + r * ldu4 + iq);
-            }
-        };
-        f32x4 xA[UB], xB[UB];
-        float wA[UB], wB[UB];
-        uint32_t mA[UB], mB[UB];
-        load(0, xA, wA, mA);
-        for (int b = 0; b < nb; b += 2) {
-            load((b + 1) * UB, xB, wB, mB);
+        for (int k = 0; k < KW; ++k)
+            ain[k] = out[(int64_t)coal(k < nk ? k : nk - 1) * ldo4 + iq];
+    };
+    if (ACC) load_acc(tile);
+    issue(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t i0 = tile * 64 + lane;
+        const int64_t iq = i0 < P4 ? i0 : P4 - 1;
+        __syncthreads();  // every wave is done reading the previous tile's t (and the tables)
+        uint32_t bad = 0;
 #pragma unroll
-            for (int u = 0; u < UB; ++u) one(xA[u], wA[u], mA[u]);
-            load((b + 2) * UB, xA, wA, mA);
-            if (b + 1 < nb) {
-#pragma unroll
-                for (int u = 0; u < UB; ++u) one(xB[u], wB[u], mB[u]);
+        for (int l = 0; l < NL; ++l) {
+            const int j = wv + W * l;
+            if (j < Ku) {
+                const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
+                f32x4 t;
+                t.x = R[l].x * wk;
+                t.y = R[l].y * wk;
+                t.z = R[l].z * wk;
+                t.w = R[l].w * wk;
+                ts[j * 64 + lane] = t;
+                bad |= (uint32_t)(__ballot(!all_in_fast_range(t)) != 0);
             }
         }
-    }
-    if (__builtin_expect(!redo, 1)) {
-        if (i0 < P4) {
+        if (lane == 0) tbad[wv] = bad;
+        f32x4 acc_in[KW];
 #pragma unroll
-            for (int s = 0; s < SB; ++s)
-                if (s < ns) out[(int64_t)(s0 + s) * ldo4 + iq] = acc[s];
-        }
-        return;
-    }
-    // slow path (acc is dead here): one coalition at a time, guarded division
-    for (int s = 0; s < ns; ++s) {
-        FastDiv d;
-        d.b = sub_total[s0 + s];
-        d.y = (float)(1.0 / (double)d.b);
-        d.fast = d.b >= 1.0f && d.b <= 2147483648.0f;
-        f32x4 a = f32x4{-0.f, -0.f, -0.f, -0.f};
-        for (int j = 0; j < Ku; ++j) {
-            if (!((member[j] >> (s0 + s)) & 1u)) continue;
-            const f32x4 x = load4<false>(Uv + (int64_t)urows[j] * ldu4 + iq);
-            const float wk = uw[j];
+        for (int k = 0; k < KW; ++k)
+            acc_in[k] = ACC ? ain[k] : f32x4{-0.f, -0.f, -0.f, -0.f};
+        // the next tile's rows (the last tile reloads itself: a static load count)
+        const int64_t next = tile + gridDim.x < ntiles ? tile + gridDim.x : tile;
+        if (ACC) load_acc(next);
+        issue(next);  // in flight during this tile's compute
+        __syncthreads();
+        uint32_t anybad = 0;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a[e] += div_exact(x[e] * wk, d);
+        for (int w = 0; w < W; ++w) anybad |= tbad[w];
+        // Common case: every t of the tile in Markstein's range and every divisor in
+        // [1, 2^31].  Otherwise (zeros, denormals, huge values, inf / nan) a compact
+        // slow path with guarded division.  Both issue exactly KW stores.
+        const bool tile_fast = fast && anybad == 0;
+        f32x4 last = acc_in[0];
+        int64_t lrow = (int64_t)coal(0) * ldo4;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            if (k < nk) {  // wave-uniform
+                const int c = coal(k);
+                f32x4 acc = acc_in[k];
+                if (__builtin_expect(tile_fast, 1)) {
+                    const f32x4 cc = cst[c];
+                    const f32x2 y2 = f32x2{cc.x, cc.y}, b2 = f32x2{cc.z, cc.w};
+                    const uint32_t vl = (uint32_t)lst[c][lane] << 10;  // lane l: member l's offset
+                    const int n = len[k];
+                    auto quot = [&](f32x4 t) {
+                        const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
+                        const f32x2 ql0 = tl * y2, qh0 = th * y2;
+                        const f32x2 ql = __builtin_elementwise_fma(
+                            __builtin_elementwise_fma(-ql0, b2, tl), y2, ql0);
+                        const f32x2 qh = __builtin_elementwise_fma(
+                            __builtin_elementwise_fma(-qh0, b2, th), y2, qh0);
+                        return f32x4{ql.x, ql.y, qh.x, qh.y};
+                    };
+                    auto tload = [&](int l) {
+                        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)vl, l);
+                        return *reinterpret_cast<const f32x4 *>(
+                            reinterpret_cast<const char *>(ts) + off + 16 * lane);
+                    };
+                    int l = 0;
+                    if (n >= 4) {
+                        // groups of 4 members: the next group's t are read from LDS
+                        // while this group's 4 independent quotients are computed;
+                        // the adds stay in member order
+                        f32x4 x0 = tload(0), x1 = tload(1), x2 = tload(2), x3 = tload(3);
+                        for (; l + 8 <= n; l += 4) {
+                            const f32x4 z0 = tload(l + 4), z1 = tload(l + 5);
+                            const f32x4 z2 = tload(l + 6), z3 = tload(l + 7);
+                            const f32x4 q0 = quot(x0), q1 = quot(x1), q2 = quot(x2), q3 = quot(x3);
+                            acc = add4(add4(add4(add4(acc, q0), q1), q2), q3);
+                            x0 = z0;
+                            x1 = z1;
+                            x2 = z2;
+                            x3 = z3;
+                        }
+                        const f32x4 q0 = quot(x0), q1 = quot(x1), q2 = quot(x2), q3 = quot(x3);
+                        acc = add4(add4(add4(add4(acc, q0), q1), q2), q3);
+                        l += 4;
+                    }
+                    for (; l < n; ++l) acc = add4(acc, quot(tload(l)));
+                } else {
+                    FastDiv d;
+                    d.b = sub_total[c];
+                    d.y = (float)(1.0 / (double)d.b);
+                    d.fast = d.b >= 1.0f && d.b <= 2147483648.0f;
+                    for (int j = 0; j < Ku; ++j) {
+                        if (!__builtin_amdgcn_readlane((int)((mj >> c) & 1ull), j)) continue;
+                        const f32x4 t = ts[j * 64 + lane];
+                        for (int e = 0; e < 4; ++e)
+                            acc[e] += (d.fast && in_fast_range(t[e])) ? markstein(t[e], d.b, d.y)
+                                                                      : t[e] / d.b;
+                    }
+                }
+                last = acc;
+                lrow = (int64_t)c * ldo4;
+            }
+            // exactly KW stores per wave and tile (past nk: the last one again; lanes
+            // past P hold column P-1's value, iq: the same bits stored twice)
+            out[lrow + iq] = last;
         }
-        if (i0 < P4) out[(int64_t)(s0 + s) * ldo4 + iq] = a;
     }
 }
 
@@ -471,14 +528,44 @@ extern "C" int dls_subset_fedavg_union_f32(const float *U, int64_t ldu, const in
                 "dls_subset_fedavg_union_f32: P, ldu, ldo must be multiples of 4");
     DLS_REQUIRE(aligned16(U) && aligned16(out), DLS_ELAYOUT,
                 "dls_subset_fedavg_union_f32: 16-byte alignment");
-    static_assert(kSubsetMaxBlock <= 1024, "at most 16 waves per block");
     const int64_t P4 = P / 4;
-    const int64_t tiles = (P4 + 63) / 64;
-    DLS_REQUIRE(tiles < (int64_t)1 << 31, DLS_EINVAL, "dls_subset_fedavg_union_f32: grid too large");
-    const int waves = (S + kSubsetSB - 1) / kSubsetSB;
-    hipLaunchKernelGGL((k_subset_union<kSubsetSB, kSubsetUB>), dim3((unsigned)tiles),
-                       dim3(64 * waves), 0, as_stream(stream), reinterpret_cast<const f32x4 *>(U),
-                       ldu / 4, urows, uweight, member, (int)Ku, sub_total, (int)S, P4,
-                       reinterpret_cast<f32x4 *>(out), ldo / 4);
-    return check_launch("dls_subset_fedavg_union_f32");
+    const int64_t ntiles = (P4 + 63) / 64;
+    hipStream_t st = as_stream(stream);
+    // unions of more than 64 clients: one launch per 64-client chunk, each
+    // continuing the running sums in `out` (the same fp32 additions, in order)
+    for (int32_t c0 = 0; c0 < Ku; c0 += kUnionChunk) {
+        const int kc = Ku - c0 < kUnionChunk ? Ku - c0 : kUnionChunk;
+        auto launch = [&](auto kern) {
+            const int64_t blocks =
+                resident_blocks(reinterpret_cast<const void *>(kern), 64 * kUnionWaves, 0);
+            const dim3 grid((unsigned)(ntiles < blocks ? ntiles : blocks));
+            hipLaunchKernelGGL(kern, grid, dim3(64 * kUnionWaves), 0, st,
+                               reinterpret_cast<const f32x4 *>(U), ldu / 4, urows + c0,
+                               uweight + c0, member + c0, kc, sub_total, (int)S, P4, ntiles,
+                               reinterpret_cast<f32x4 *>(out), ldo / 4);
+        };
+        const int kw = (S + kUnionWaves - 1) / kUnionWaves;
+        static_assert(DLS_SUBSET_UNION_MAX == 8 * kUnionWaves, "KW instances 1..8");
+#define DLS_UNION_KW(K_)                                                 \
+    case K_:                                                             \
+        if (c0 == 0)                                                     \
+            launch(k_subset_union<K_, false>);                           \
+        else /* a later chunk continues the running sums in `out` */    \
+            launch(k_subset_union<K_, true>);                            \
+        break;
+        switch (kw) {
+            DLS_UNION_KW(1)
+            DLS_UNION_KW(2)
+            DLS_UNION_KW(3)
+            DLS_UNION_KW(4)
+            DLS_UNION_KW(5)
+            DLS_UNION_KW(6)
+            DLS_UNION_KW(7)
+            DLS_UNION_KW(8)
+        }
+#undef DLS_UNION_KW
+        const int rc = check_launch("dls_subset_fedavg_union_f32");
+        if (rc != DLS_OK) return rc;
+    }
+    return DLS_OK;
 }

@@ -342,19 +342,21 @@ def test_int8_symmetric_per_channel_quantize_golden():
 
 
 def test_segment_minmax_ignores_nan():
-    """NaNs are ignored (dls_hip.h) on both the bulk and the segment-boundary path."""
+    """NaNs are ignored (dls_hip.h) on both the bulk and the segment-boundary path;
+    an all-NaN segment keeps the identities (+inf, -inf)."""
     from distributed_learning_simulator_amd import _native
-    sizes = [5, 8190, 3, 9000, 1]
+    sizes = [5, 8190, 3, 9000, 1, 2]
     off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     g = torch.Generator().manual_seed(3)
     x = torch.rand(int(off[-1]), generator=g) + 0.5  # all positive
-    x[off[:-1] + 1 - (np.array(sizes) == 1)] = float("nan")  # one NaN per segment
-    x[8192:8200] = float("nan")  # inside a boundary-crossing chunk
-    x[-1] = 0.75  # the 1-element segment keeps a value
+    x[torch.from_numpy(off[:4] + 1)] = float("nan")  # one NaN in each of the first 4 segments
+    x[8185:8194] = float("nan")  # segment 1, across the 8192-element block boundary
+    x[int(off[5]):] = float("nan")  # the last segment is all NaN
     mins = torch.empty(len(sizes), device=dev)
     maxs = torch.empty(len(sizes), device=dev)
     _native.segment_minmax(x.to(dev), torch.from_numpy(off).to(dev), int(off[-1]), mins, maxs)
-    for s in range(len(sizes)):
+    for s in range(len(sizes) - 1):
         part = x[off[s]:off[s + 1]]
         part = part[~torch.isnan(part)]
         assert float(mins[s]) == float(part.min()) and float(maxs[s]) == float(part.max()), s
+    assert float(mins[-1]) == float("inf") and float(maxs[-1]) == float("-inf")

@@ -73,64 +73,66 @@ def setup(dev, want=()):
         t1 = float(w1.sum())
         W["fedavg1k"] = (lambda L: L.dls_fedavg_f32(ptr(U1), P, ptr(r1), ptr(w1), 1000, t1, P, 0,
                                                     ptr(out), stream()), 1000 * P * 4 + P * 4)
-    Wd = _native.sign_words(P)
-    planes = torch.randint(-2**62, 2**62, (1000, Wd), generator=g, device=dev)
-    planes[:, 1::2] &= ~planes[:, 0::2]
-    so = torch.empty(P, device=dev)
-    cnt = torch.empty(P, dtype=torch.int32, device=dev)
-    W["vote"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, ptr(cnt), ptr(so),
-                                           None, stream()), 1000 * Wd * 8 + 2 * P * 4)
-    vp = torch.empty(Wd, dtype=torch.int64, device=dev)
-    W["vote_sign"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, None, ptr(so),
-                                                ptr(vp), stream()), 1000 * Wd * 8 + P * 4 + Wd * 8)
-    X = torch.sign(torch.randn((16, P), generator=g, device=dev))
-    pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
-    W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
-                 16 * (P * 4 + Wd * 8))
-    from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
-    template = {}
-    for name, s in vgg16():
-        if len(s) >= 2:
-            template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
-                              torch.zeros(s[0], dtype=torch.int64))
-        else:
-            template[name] = torch.zeros(s)
-    st = QuantizedClientStore(template, dev, capacity=100)
-    st.Q.random_(0, 256, generator=g)
-    st.F.normal_(generator=g)
-    st.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
-    st.sz[..., 1].zero_()
-    qo = torch.empty(st.layout.P, device=dev)
-    ql = st.qlayout
-    Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
-    Pf = sum(m for m, k in zip(st.layout.numels, ql.kinds) if not k)
-    W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast), ptr(st.Q), st.Q.stride(0),
-                                                 ptr(st.F), st.F.stride(0), ptr(st.sz),
-                                                 st.sz.stride(1) // 2, st.sz.stride(0) // 2,
-                                                 ptr(rows), ptr(w), 100, tot,
-                                                 ptr(qo), stream()),
-                  100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
-    # the same payloads with 1 KiB tiles only (FAST_TILE = TILE): the single-slice
-    # kernel path, and the only tiling a library from before multi-KiB tiles handles
-    from distributed_learning_simulator_amd import quant_store as qs
-    saved, qs.FAST_TILE = qs.FAST_TILE, qs.TILE
-    qt1, nf1 = ql.tiles()
-    qs.FAST_TILE = saved
-    tiles1 = torch.from_numpy(qt1.view(np.uint8).copy()).to(dev)
-    W["quant1k"] = (lambda L: L.dls_dequant_fedavg(ptr(tiles1), len(qt1), nfast_arg(L, nf1), ptr(st.Q),
-                                                   st.Q.stride(0), ptr(st.F), st.F.stride(0),
-                                                   ptr(st.sz), st.sz.stride(1) // 2,
-                                                   st.sz.stride(0) // 2, ptr(rows), ptr(w), 100,
-                                                   tot, ptr(qo), stream()),
-                    100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
-    rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
-    W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast),
-                                                         ptr(st.Q), st.Q.stride(0),
-                                                         ptr(st.F), st.F.stride(0), ptr(st.sz),
-                                                         st.sz.stride(1) // 2,
-                                                         st.sz.stride(0) // 2, ptr(rows0), ptr(w),
-                                                         100, tot, ptr(qo), stream()),
-                          100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+    if {"vote", "vote_sign", "pack"} & set(want):
+        Wd = _native.sign_words(P)
+        planes = torch.randint(-2**62, 2**62, (1000, Wd), generator=g, device=dev)
+        planes[:, 1::2] &= ~planes[:, 0::2]
+        so = torch.empty(P, device=dev)
+        cnt = torch.empty(P, dtype=torch.int32, device=dev)
+        W["vote"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, ptr(cnt), ptr(so),
+                                               None, stream()), 1000 * Wd * 8 + 2 * P * 4)
+        vp = torch.empty(Wd, dtype=torch.int64, device=dev)
+        W["vote_sign"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, None, ptr(so),
+                                                    ptr(vp), stream()), 1000 * Wd * 8 + P * 4 + Wd * 8)
+        X = torch.sign(torch.randn((16, P), generator=g, device=dev))
+        pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
+        W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
+                     16 * (P * 4 + Wd * 8))
+    if {"quant", "quant1k", "quant_samerow"} & set(want):
+        from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
+        template = {}
+        for name, s in vgg16():
+            if len(s) >= 2:
+                template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
+                                  torch.zeros(s[0], dtype=torch.int64))
+            else:
+                template[name] = torch.zeros(s)
+        st = QuantizedClientStore(template, dev, capacity=100)
+        st.Q.random_(0, 256, generator=g)
+        st.F.normal_(generator=g)
+        st.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
+        st.sz[..., 1].zero_()
+        qo = torch.empty(st.layout.P, device=dev)
+        ql = st.qlayout
+        Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
+        Pf = sum(m for m, k in zip(st.layout.numels, ql.kinds) if not k)
+        W["quant"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast), ptr(st.Q), st.Q.stride(0),
+                                                     ptr(st.F), st.F.stride(0), ptr(st.sz),
+                                                     st.sz.stride(1) // 2, st.sz.stride(0) // 2,
+                                                     ptr(rows), ptr(w), 100, tot,
+                                                     ptr(qo), stream()),
+                      100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+        # the same payloads with 1 KiB tiles only (FAST_TILE = TILE): the single-slice
+        # kernel path, and the only tiling a library from before multi-KiB tiles handles
+        from distributed_learning_simulator_amd import quant_store as qs
+        saved, qs.FAST_TILE = qs.FAST_TILE, qs.TILE
+        qt1, nf1 = ql.tiles()
+        qs.FAST_TILE = saved
+        tiles1 = torch.from_numpy(qt1.view(np.uint8).copy()).to(dev)
+        W["quant1k"] = (lambda L: L.dls_dequant_fedavg(ptr(tiles1), len(qt1), nfast_arg(L, nf1), ptr(st.Q),
+                                                       st.Q.stride(0), ptr(st.F), st.F.stride(0),
+                                                       ptr(st.sz), st.sz.stride(1) // 2,
+                                                       st.sz.stride(0) // 2, ptr(rows), ptr(w), 100,
+                                                       tot, ptr(qo), stream()),
+                        100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+        rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
+        W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast),
+                                                             ptr(st.Q), st.Q.stride(0),
+                                                             ptr(st.F), st.F.stride(0), ptr(st.sz),
+                                                             st.sz.stride(1) // 2,
+                                                             st.sz.stride(0) // 2, ptr(rows0), ptr(w),
+                                                             100, tot, ptr(qo), stream()),
+                              100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
     # Shapley default path: 50 coalitions (members with p = 1/2) over 50 clients,
     # each client row read once per batch (dls_subset_fedavg_union_f32)
     from distributed_learning_simulator_amd.aggregation import union_batch
@@ -172,6 +174,7 @@ def main():
     ap.add_argument("--workloads", default="fedavg,vote,quant,gemm,pack")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
+    ap.add_argument("--only-run", action="store_true", help="just launch (rocprofv3 target)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -183,6 +186,13 @@ def main():
     res = {}
     for wl in args.workloads.split(","):
         fn, nbytes = W[wl]
+        if args.only_run:  # a profiler target: the first variant only, launches back to back
+            L = next(iter(libs.values()))
+            for _ in range(args.launches):
+                assert fn(L) == 0
+            torch.cuda.synchronize()
+            print(wl, "ran", args.launches, flush=True)
+            continue
         times = {v: [] for v in libs}
         for name, L in libs.items():  # warm (and check status)
             rc = fn(L)
