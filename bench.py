@@ -413,10 +413,9 @@ def bench_shapley_exact(args, dev):
     wall, kms = timed_launches(step, args.steps, args.warmup)
     ms = wall / args.steps * 1e3
     pairs = sum(len(c) for c in subs)
-    waves = -(-S // 8)
     # minimum VALU lane-ops: per parameter, 4 per (client, coalition) membership
-    # (Markstein q0, r, q + the add) and 4/4 per (client, wave) for t = x * n_i
-    valu_ops = layout.numel * (4 * pairs + K * waves)
+    # (Markstein q0, r, q + the add) and 1 per client for t = x * n_i
+    valu_ops = layout.numel * (4 * pairs + K)
     bytes_per_launch = (K + S) * P * 4
     # the per-coalition kernel on the same batch, for comparison
     off, fr, fw, ft = [0], [], [], []
