@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("DLS_HIP_LIB", os.path.join(_HERE, "libdls_hip.so"))
 FEDAVG_EXACT = 0
 FEDAVG_FMA = 1
 SIGN_NAN_MARK = 1 << 24
+QTILE_GROUPS = 9  # DLS_QTILE_GROUPS
 SUBSET_UNION_MAX = 64  # DLS_SUBSET_UNION_MAX: coalitions per dls_subset_fedavg_union_f32 call
 
 
@@ -212,11 +213,12 @@ def sign_sgd_apply(param, vote_planes, neg_lr, weight_decay, stream=None):
 # ----------------------------------------------------------------------- quant
 def dequant_fedavg(tiles, ntiles, nfast, Q, F, sz, rows, weight, total, out, sz_strides=None,
                    stream=None):
-    """nfast: 4 counts of one-channel tiles with 4, 3, 2, 1 KiB slices at the head of
-    the table (quant_store.QuantLayout.tiles()); sz: (scale, zero point) pairs;
+    """nfast: the QTILE_GROUPS counts of grouped tiles at the head of the table
+    (quant_store.QuantLayout.tiles()); sz: (scale, zero point) pairs;
     sz_strides = (row, channel) strides in pairs (default: a channel-major
     [C+1, capacity, 2] tensor)."""
-    nf = (ctypes.c_int32 * 4)(*[int(x) for x in nfast])
+    assert len(nfast) == QTILE_GROUPS
+    nf = (ctypes.c_int32 * QTILE_GROUPS)(*[int(x) for x in nfast])
     if sz_strides is None:
         sz_strides = (sz.stride(1) // 2, sz.stride(0) // 2)
     _check(lib().dls_dequant_fedavg(_ptr(tiles), ntiles, nf, _ptr(Q),

@@ -35,9 +35,9 @@ int check_launch(const char *what);
 // Blocks of `kernel` resident on the whole device at once (occupancy x CUs),
 // for persistent grids; cached per (kernel, device, block, lds).
 int resident_blocks(const void *kernel, int block, size_t lds);
-// Auxiliary stream on `parent`'s device for fork/join inside one C-ABI call
-// (nullptr on error).
-hipStream_t side_stream(hipStream_t parent);
+// Auxiliary stream number idx (0..63) on `parent`'s device for fork/join inside
+// one C-ABI call (nullptr on error).
+hipStream_t side_stream(hipStream_t parent, int idx);
 
 inline hipStream_t as_stream(dls_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }

@@ -59,8 +59,8 @@ int resident_blocks(const void *kernel, int block, size_t lds) {
     return n;
 }
 
-hipStream_t side_stream(hipStream_t parent) {
-    // one non-blocking stream per device, created on first use and kept for the
+hipStream_t side_stream(hipStream_t parent, int idx) {
+    // non-blocking streams per (device, idx), created on first use and kept for the
     // process (the library's launchers fork small concurrent kernels onto it and
     // join back to the caller's stream before returning).  The device is the
     // parent stream's, not the calling thread's current device: worker threads
@@ -69,8 +69,9 @@ hipStream_t side_stream(hipStream_t parent) {
     static std::unordered_map<int, hipStream_t> streams;
     int dev = 0;
     if (hipStreamGetDevice(parent, &dev) != hipSuccess) return nullptr;
+    const int key = dev * 64 + idx;
     std::lock_guard<std::mutex> g(mu);
-    auto it = streams.find(dev);
+    auto it = streams.find(key);
     if (it != streams.end()) return it->second;
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
@@ -79,7 +80,7 @@ hipStream_t side_stream(hipStream_t parent) {
     const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (cur != dev) (void)hipSetDevice(cur);
     if (e != hipSuccess) return nullptr;
-    streams[dev] = s;
+    streams[key] = s;
     return s;
 }
 

@@ -19,6 +19,10 @@ constexpr int kBlock = 256;
 constexpr int kQuantU = 2;      // clients per batch (1 KiB tiles); two batches in flight per lane
 constexpr int kQuantUG = 1;     // clients per batch on multi-KiB tiles
 constexpr int kQuantSched = 2;  // element pairs between scheduling barriers
+#ifndef DLS_LANE_U
+#define DLS_LANE_U 2
+#endif
+constexpr int kLaneU = DLS_LANE_U;  // clients per batch on lane-channel tiles
 
 __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
     return (float)((w >> (8 * k)) & 0xffu);  // selects v_cvt_f32_ubyte{k}
@@ -274,29 +278,54 @@ __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_
     cr.init(rows, w, K);
     const float zadj = SIGNED ? 128.f : 0.f;
     const bool two = split < 16;
+    struct One {
+        u32x4 qv;
+        f32x2 a, b;
+        float wk;
+    };
+    constexpr int U = 4;  // clients per batch, double-buffered (a latency chain otherwise)
+    struct Batch {
+        One c[U];
+    };
     for (int base = 0; base < K; base += 64) {
         const int tr = cr.r0;
         const float tw = cr.w0;
         cr.advance(rows, w, K, base);
-        const int n = min(64, K - base);
-        for (int j = 0; j < n; ++j) {
+        auto fetch = [&](int j, One &o) {
             const int64_t r = readlane_i(tr, j);
-            const float wk = readlane_f(tw, j);
-            u32x4 qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
-            if (SIGNED) qv ^= 0x80808080u;
-            const f32x2 a = szc[r * L.row];
-            const f32x2 b = two ? szc[r * L.row + L.chan] : a;
-            const float za = a.y + zadj, zb = b.y + zadj;
-            const bool fast = d.fast && scale_fast(a.x * wk) && scale_fast(b.x * wk);
+            o.wk = readlane_f(tw, j);
+            o.qv = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(Qt + r * ldq));
+            o.a = szc[r * L.row];
+            o.b = two ? szc[r * L.row + L.chan] : o.a;
+        };
+        auto step = [&](One o) {
+            if (SIGNED) o.qv ^= 0x80808080u;
+            const float za = o.a.y + zadj, zb = o.b.y + zadj;
+            const bool fast = d.fast && scale_fast(o.a.x * o.wk) && scale_fast(o.b.x * o.wk);
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const bool second = e >= split;
-                const float s = second ? b.x : a.x;
+                const float s = second ? o.b.x : o.a.x;
                 const float z = second ? zb : za;
-                const float t = ((byte_f32(qv[e >> 2], e & 3) - z) * s) * wk;
+                const float t = ((byte_f32(o.qv[e >> 2], e & 3) - z) * s) * o.wk;
                 acc[e] += fast ? markstein(t, d.b, d.y) : t / d.b;
             }
-        }
+        };
+        chunk_pipeline<U, Batch>(
+            min(64, K - base),
+            [&](int j0, Batch &bt) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) fetch(j0 + u, bt.c[u]);
+            },
+            [&](const Batch &bt) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) step(bt.c[u]);
+            },
+            [&](int j) {
+                One o;
+                fetch(j, o);
+                step(o);
+            });
     }
 }
 
@@ -446,6 +475,10 @@ __device__ __forceinline__ void store16(const WaveTile &wt, float (&acc)[16],
         o[v] = f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
 }
 
+template <int G>
+__device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][16],
+                                           float *__restrict__ out);
+
 // One-channel tiles of up to 4 KiB: slice g of the tile is lanes'
 // 16-element chunks 1024 g + 16 lane; the wave walks the clients once for all
 // its slices (per-client table reads and readlanes amortised over G KiB).
@@ -466,7 +499,106 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
         qoff[g] = (uint32_t)(wt.t.src + (e0 < wt.lenpad ? e0 : wt.lenpad - 16));  // ldq < 4 GiB
     }
     int_one_channel<SIGNED, G, TWO>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
-    // transpose through LDS so that each store instruction writes 1 KiB contiguous
+    store_tile<G>(wt, acc, out);
+}
+
+// Multi-channel tiles of up to 4 KiB (every int tensor whose channel rows are a
+// multiple of 16 elements, so no lane's 16-element chunk straddles two channels:
+// the 3x3 convs of ResNet-18 / VGG-16, 576-4608-element rows).  Slice g of the
+// tile is lanes' chunks 1024 g + 16 lane, each lane in its own channel, so every
+// client step loads the lane's (scale, zero point) per slice beside its payload
+// (8 B, a few distinct lines per wave); the wave walks the clients once for all
+// its slices, double-buffered like the one-channel tiles.
+template <bool SIGNED, int G, bool TWO>
+__device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
+                                          int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
+                                          const int32_t *__restrict__ rows,
+                                          const float *__restrict__ w, int K, const FastDiv &d,
+                                          float *__restrict__ out) {
+    float acc[G][16];
+    uint32_t qoff[G];
+    int64_t coff[G];  // the lane's channel in slice g, in (scale, zp) pairs
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[g][e] = -0.f;
+        const int e0 = 1024 * g + 16 * __lane_id();
+        const int ec = e0 < wt.lenpad ? e0 : wt.lenpad - 16;  // idle lanes: a valid duplicate
+        qoff[g] = (uint32_t)(wt.t.src + ec);
+        const int c = min(wt.t.chan0 + (wt.t.row_pos + ec) / wt.t.row_len, wt.t.chan_end - 1);
+        coff[g] = (int64_t)c * L.chan;
+    }
+    struct One {
+        u32x4 qv[G];
+        f32x2 s[G];
+        float wk;
+    };
+    struct Batch {
+        One c[kLaneU];
+    };
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        cr.advance(rows, w, K, base);
+        auto fetch = [&](int j, One &b) {
+            const int64_t r = readlane_i(tr, j);
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+                b.s[g] = sz[coff[g] + r * L.row];
+            }
+            b.wk = readlane_f(tw, j);
+        };
+        auto step = [&](const One &b) {
+            // one wave-uniform decision per client: exact fl(zp * s) and the fast
+            // division range on every lane and slice (always, for symmetric int8)
+            int ok = d.fast;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float zs = b.s[g].y * b.s[g].x;
+                ok &= (int)(__builtin_fmaf(b.s[g].y, b.s[g].x, -zs) == 0.f) &
+                      (int)scale_fast(b.s[g].x * b.wk);
+            }
+            if (__builtin_expect(__ballot(!ok) == 0, 1)) {
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    accum16_one<true, true, SIGNED, TWO>(acc[g], b.qv[g], b.s[g].x,
+                                                         b.s[g].y * b.s[g].x, 0.f, b.wk, d);
+            } else {  // rare clients: the reference's formula with IEEE division
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    accum16_one<false, false, SIGNED>(acc[g], b.qv[g], b.s[g].x, 0.f, b.s[g].y,
+                                                      b.wk, d);
+            }
+        };
+        chunk_pipeline<kLaneU, Batch>(
+            min(64, K - base),
+            [&](int j0, Batch &b) {
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) fetch(j0 + u, b.c[u]);
+            },
+            [&](const Batch &b) {
+#pragma unroll
+                for (int u = 0; u < kLaneU; ++u) step(b.c[u]);
+            },
+            [&](int j) {
+                One b;
+                fetch(j, b);
+                step(b);
+            });
+    }
+    store_tile<G>(wt, acc, out);
+}
+
+// Write a wave tile's G slices of accumulators, transposed through LDS so that
+// each store instruction writes 1 KiB contiguous.
+template <int G>
+__device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][16],
+                                           float *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
     float *mine = xs[threadIdx.x >> 6];
 #pragma unroll
@@ -503,6 +635,84 @@ __global__ __launch_bounds__(kBlock, 1) void k_dequant_fast(
         fast_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
     else
         fast_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+}
+
+// fp32 tensors (biases, norm weights) as their own group: tiles of <= 256
+// elements, a lane owning 4, walked like dls_fedavg_f32's pipelined kernel —
+// batches of kF32U clients double-buffered — so that the few waves of a small
+// tensor keep 2 * kF32U client rows in flight instead of one dependent load per
+// client (with K = 1000 clients the unpipelined loop is a ~2 ms latency chain).
+constexpr int kF32U = 8;
+__global__ __launch_bounds__(kBlock) void k_dequant_f32(const dls_qtile *__restrict__ tiles,
+                                                        int ntiles, const float *__restrict__ F,
+                                                        int64_t ldf,
+                                                        const int32_t *__restrict__ rows,
+                                                        const float *__restrict__ w, int K,
+                                                        FastDiv d, float *__restrict__ out) {
+    const int idx = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (idx >= ntiles) return;  // wave-uniform
+    const dls_qtile t = tiles[idx];
+    const int e0 = 4 * __lane_id();
+    const int lenpad = (t.len + 63) & ~63;
+    const int ec = e0 < lenpad ? e0 : lenpad - 4;  // idle lanes load a valid duplicate
+    const float *src = F + t.src + ec;
+    f32x4 acc = f32x4{-0.f, -0.f, -0.f, -0.f};
+    auto term = [&](f32x4 x, float wk) {
+        f32x4 q;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) q[c] = div_exact(x[c] * wk, d);
+        return q;
+    };
+    struct Batch {
+        f32x4 x[kF32U];
+        float wk[kF32U];
+    };
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        cr.advance(rows, w, K, base);
+        auto fetch = [&](int j, f32x4 &x, float &wk) {
+            const int64_t r = readlane_i(tr, j);
+            x = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(src + r * ldf));
+            wk = readlane_f(tw, j);
+        };
+        chunk_pipeline<kF32U, Batch>(
+            min(64, K - base),
+            [&](int j0, Batch &b) {
+#pragma unroll
+                for (int u = 0; u < kF32U; ++u) fetch(j0 + u, b.x[u], b.wk[u]);
+            },
+            [&](const Batch &b) {
+#pragma unroll
+                for (int u = 0; u < kF32U; ++u) acc = acc + term(b.x[u], b.wk[u]);
+            },
+            [&](int j) {
+                f32x4 x;
+                float wk;
+                fetch(j, x, wk);
+                acc = acc + term(x, wk);
+            });
+    }
+    if (e0 < lenpad) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = e0 + c < t.len ? acc[c] : 0.f;  // keep padding zero
+        *reinterpret_cast<f32x4 *>(out + t.dst + e0) = acc;
+    }
+}
+
+template <int G, bool TWO>
+__global__ __launch_bounds__(kBlock, 1) void k_dequant_lanes(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
+    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
+    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    if (wt.t.kind == 1)
+        lane_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+    else
+        lane_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
@@ -733,12 +943,12 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     DLS_REQUIRE(tiles && nfast && rows && weight && out && sz, DLS_EINVAL,
                 "dls_dequant_fedavg: null pointer");
     int64_t nf = 0;
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < DLS_QTILE_GROUPS; ++g) {
         DLS_REQUIRE(nfast[g] >= 0, DLS_EINVAL, "dls_dequant_fedavg: nfast[%d]=%d", g, nfast[g]);
         nf += nfast[g];
     }
     DLS_REQUIRE(ntiles > 0 && K > 0 && nf <= ntiles, DLS_EINVAL,
-                "dls_dequant_fedavg: ntiles=%d fast tiles=%lld K=%d", ntiles, (long long)nf, K);
+                "dls_dequant_fedavg: ntiles=%d grouped tiles=%lld K=%d", ntiles, (long long)nf, K);
     DLS_REQUIRE(ldq % 16 == 0 && ldf % 4 == 0 && aligned16(out) && (!Q || aligned16(Q)) &&
                     (!F || aligned16(F)),
                 DLS_ELAYOUT, "dls_dequant_fedavg: ldq %% 16, ldf %% 4, 16-byte alignment");
@@ -750,63 +960,101 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
-    // The widest non-empty group carries the bulk of the bytes; the other groups
-    // and the general tiles are small grids whose waves are latency-bound
-    // (100+ dependent client steps each), so they run on a side stream,
-    // concurrently with the bulk kernel, and the caller's stream joins them.
-    const dls_qtile *tg[4];
+    // Groups: 0-3 one-channel tiles of 4/3/2/1 KiB slices, 4-7 lane-channel tiles
+    // of 4/3/2/1 slices, 8 fp32 tiles, then the general tiles.  The group with
+    // the most bytes runs on the caller's stream; every other non-empty group on a
+    // side stream of its own, concurrently (their waves walk all K clients, so a
+    // small group is a long latency chain, not a small amount of work), and the
+    // caller's stream joins them all.
+    const dls_qtile *tg[DLS_QTILE_GROUPS];
     const dls_qtile *t = tiles;
     int big = -1;
-    for (int g = 0; g < 4; ++g) {
+    auto bytes = [&](int g) {  // ~ bytes per client of group g
+        return g < 8 ? (int64_t)nfast[g] * 1024 * (4 - g % 4) : (int64_t)nfast[g] * 1024;
+    };
+    for (int g = 0; g < DLS_QTILE_GROUPS; ++g) {
         tg[g] = t;
         t += nfast[g];
-        if (big < 0 && nfast[g] > 0) big = g;
+        if (nfast[g] > 0 && (big < 0 || bytes(g) > bytes(big))) big = g;
     }
     const int ngen = ntiles - (int)nf;
-    const int64_t small_tiles = nf - (big >= 0 ? nfast[big] : 0) + ngen;
-    hipStream_t side = st;
-    hipEvent_t fork = nullptr, join = nullptr;
-    if (big >= 0 && small_tiles > 0) {
-        hipStream_t s2 = side_stream(st);
-        if (s2 && hipEventCreateWithFlags(&fork, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&join, hipEventDisableTiming) == hipSuccess &&
-            hipEventRecord(fork, st) == hipSuccess && hipStreamWaitEvent(s2, fork, 0) == hipSuccess)
-            side = s2;
-    }
-    auto launch_fast = [&](int g, hipStream_t s) {
+    hipEvent_t fork = nullptr;
+    hipEvent_t joins[DLS_QTILE_GROUPS + 1] = {};
+    hipStream_t sides[DLS_QTILE_GROUPS + 1] = {};
+    int nside = 0;
+    bool forked = false;
+    auto stream_for = [&](bool empty) -> hipStream_t {  // a fresh side stream, else st
+        if (empty) return st;
+        if (!forked) {
+            forked = true;
+            if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(fork, st) != hipSuccess) {
+                if (fork) (void)hipEventDestroy(fork);
+                fork = nullptr;
+            }
+        }
+        if (!fork) return st;
+        hipStream_t s2 = side_stream(st, nside);
+        if (!s2 || hipStreamWaitEvent(s2, fork, 0) != hipSuccess) return st;
+        sides[nside++] = s2;
+        return s2;
+    };
+    using Kfn = void (*)(const dls_qtile *, int, const uint8_t *, int64_t, const f32x2 *, SzLayout,
+                         const int32_t *, const float *, int, FastDiv, float *);
+    static const Kfn kgroup[8][2] = {
+        {k_dequant_fast<4, false>, k_dequant_fast<4, true>},
+        {k_dequant_fast<3, false>, k_dequant_fast<3, true>},
+        {k_dequant_fast<2, false>, k_dequant_fast<2, true>},
+        {k_dequant_fast<1, false>, k_dequant_fast<1, true>},
+        {k_dequant_lanes<4, false>, k_dequant_lanes<4, true>},
+        {k_dequant_lanes<3, false>, k_dequant_lanes<3, true>},
+        {k_dequant_lanes<2, false>, k_dequant_lanes<2, true>},
+        {k_dequant_lanes<1, false>, k_dequant_lanes<1, true>}};
+    // A wave walks all K clients, so waves are long and equal: a group is launched
+    // in pieces of at most one generation of resident waves (a last generation of
+    // a few waves would run alone at latency-bound speed; cf. dls_fedavg_f32).
+    auto launch_group = [&](int g, hipStream_t s) {
         const int n = nfast[g];
         if (n == 0) return;
-        const dim3 grid((unsigned)((n + wpb - 1) / wpb));
-        using Kfn = void (*)(const dls_qtile *, int, const uint8_t *, int64_t, const f32x2 *,
-                             SzLayout, const int32_t *, const float *, int, FastDiv, float *);
-        static const Kfn kfast[4][2] = {{k_dequant_fast<4, false>, k_dequant_fast<4, true>},
-                                        {k_dequant_fast<3, false>, k_dequant_fast<3, true>},
-                                        {k_dequant_fast<2, false>, k_dequant_fast<2, true>},
-                                        {k_dequant_fast<1, false>, k_dequant_fast<1, true>}};
-        hipLaunchKernelGGL(kfast[g][d.two ? 1 : 0], grid, dim3(kBlock), 0, s, tg[g], n,
-                           reinterpret_cast<const uint8_t *>(Q), ldq,
-                           reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
+        if (g == 8) {
+            hipLaunchKernelGGL(k_dequant_f32, dim3((unsigned)((n + wpb - 1) / wpb)), dim3(kBlock),
+                               0, s, tg[g], n, F, ldf, rows, weight, (int)K, d, out);
+            return;
+        }
+        const Kfn kern = kgroup[g][d.two ? 1 : 0];
+        const int64_t slots = (int64_t)resident_blocks(reinterpret_cast<const void *>(kern), kBlock,
+                                                       0) * wpb;
+        const int64_t np = (n + slots - 1) / slots;
+        const int64_t per = (n + np - 1) / np;  // tiles per piece, <= slots
+        for (int64_t t0 = 0; t0 < n; t0 += per) {
+            const int m = (int)(n - t0 < per ? n - t0 : per);
+            hipLaunchKernelGGL(kern, dim3((unsigned)((m + wpb - 1) / wpb)), dim3(kBlock), 0, s,
+                               tg[g] + t0, m, reinterpret_cast<const uint8_t *>(Q), ldq,
+                               reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
+        }
     };
-    for (int g = 0; g < 4; ++g)
-        if (g != big) launch_fast(g, side);
+    for (int g = 0; g < DLS_QTILE_GROUPS; ++g)
+        if (g != big && nfast[g] > 0) launch_group(g, stream_for(false));
     if (ngen > 0)
         hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
-                           dim3(kBlock), 0, side, t, ngen,
+                           dim3(kBlock), 0, stream_for(false), t, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
-    if (big >= 0) launch_fast(big, st);
+    if (big >= 0) launch_group(big, st);
     int rc = check_launch("dls_dequant_fedavg");
-    if (side != st) {
-        hipError_t e = hipEventRecord(join, side);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, join, 0);
+    for (int i = 0; i < nside; ++i) {
+        hipError_t e = hipEventCreateWithFlags(&joins[i], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(joins[i], sides[i]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, joins[i], 0);
         if (e != hipSuccess) {  // the caller's stream must not run ahead of the side work
-            (void)hipStreamSynchronize(side);
+            (void)hipStreamSynchronize(sides[i]);
             set_error("dls_dequant_fedavg: stream join failed: %s", hipGetErrorString(e));
             rc = (int)e;
         }
     }
+    for (int i = 0; i < nside; ++i)
+        if (joins[i]) (void)hipEventDestroy(joins[i]);
     if (fork) (void)hipEventDestroy(fork);  // released once the enqueued record / wait complete
-    if (join) (void)hipEventDestroy(join);
     return rc;
 }
 

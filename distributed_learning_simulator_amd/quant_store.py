@@ -28,6 +28,9 @@ from .layout import ALIGN, ParameterLayout, _round_up
 
 TILE = 1024  # one wavefront slice: 64 lanes x 16 elements
 FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
+LANE_TILE = 1024  # multi-channel tiles (channel rows a multiple of 16): slices per wavefront
+F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
+FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
 QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
 
 QTILE_DTYPE = np.dtype([("dst", "<i8"), ("src", "<i8"), ("len", "<i4"), ("kind", "<i4"),
@@ -97,26 +100,43 @@ class QuantLayout:
         return True
 
     def tiles(self):
-        """(table, nfast): wave tiles, one-channel int tiles first, grouped by their
-        number of 1 KiB slices (nfast = their counts for 4, 3, 2, 1 slices).
+        """(table, nfast): wave tiles; nfast = counts of the 8 grouped kinds at the
+        head of the table (dls_hip.h DLS_QTILE_GROUPS), then the general tiles.
 
-        int tensors whose channel rows are long (>= 1024, multiple of 64) and
-        fill 1 KiB slices well get channel-aligned tiles of up to FAST_TILE
-        elements (a wave streams up to 4 KiB of every client row); every other
-        tensor is cut into TILE-element tiles from its start."""
-        rows = []
+        * one-channel tiles (groups 0-3: 4, 3, 2, 1 KiB slices): int tensors whose
+          channel rows are long (>= 1024, multiple of 64) and fill 1 KiB slices
+          well get channel-aligned tiles of up to FAST_TILE elements (a wave
+          streams up to 4 KiB of every client row with one (scale, zp) per client);
+        * lane-channel tiles (groups 4-7): the other int tensors whose channel rows
+          are a multiple of 16 elements (no lane's 16-element chunk straddles two
+          channels: 3x3 convs, fc layers) are cut into LANE_TILE-element tiles from
+          their start, each lane loading its own channel's (scale, zp);
+        * fp32 tiles (group 8, <= F32_TILE elements): the fp32 tensors;
+        * general tiles (<= TILE elements): the remaining int tensors (rows
+          shorter than 16 or not a multiple of 16)."""
+        rows, lane_rows, f32_rows = [], [], []
         for i, kind in enumerate(self.kinds):
             n = self.layout.numels[i]
             rl = self.row_len[i]
             off, src, cb = self.layout.offsets[i], self.src[i], self.chan_base[i]
             cend = cb + self.channels[i] if kind else 0
             waste = -rl % TILE  # idle lanes of the row's last slice
-            if kind and rl >= TILE and rl % 64 == 0 and 8 * waste <= rl:
+            if kind and rl >= TILE and rl % 64 == 0 and (
+                    waste == 0 if FAST_WASTE == 0 else FAST_WASTE * waste <= rl):
                 for c in range(self.channels[i]):
                     for j in range(0, rl, FAST_TILE):
                         e = c * rl + j
                         rows.append((off + e, src + e, min(FAST_TILE, rl - j), kind, cb + c, rl,
                                      j, cend))
+                continue
+            if kind and rl % 16 == 0:
+                for e in range(0, n, LANE_TILE):
+                    lane_rows.append((off + e, src + e, min(LANE_TILE, n - e), kind, cb + e // rl,
+                                      rl, e % rl, cend))
+                continue
+            if not kind:
+                for e in range(0, n, F32_TILE):
+                    f32_rows.append((off + e, src + e, min(F32_TILE, n - e), 0, 0, 1, 0, 0))
                 continue
             for e in range(0, n, TILE):
                 rows.append((off + e, src + e, min(TILE, n - e), kind, cb + e // rl if kind else 0,
@@ -129,6 +149,8 @@ class QuantLayout:
             return (r[2] + 63) // 64 * 64 // TILE + ((r[2] + 63) // 64 * 64 % TILE != 0)
 
         fast = [[r for r in rows if one_channel(r) and slices(r) == g] for g in (4, 3, 2, 1)]
+        fast += [[r for r in lane_rows if slices(r) == g] for g in (4, 3, 2, 1)]
+        fast += [f32_rows]
         rest = [r for r in rows if not one_channel(r)]
         assert all(r[2] <= TILE for r in rest)
         return (np.array([r for grp in fast for r in grp] + rest, dtype=QTILE_DTYPE),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DLS_ABI_VERSION 1
+#define DLS_ABI_VERSION 2
 
 #define DLS_OK 0
 #define DLS_EINVAL (-1)     /* bad size / null pointer / unsupported mode */
@@ -164,7 +164,7 @@ int dls_sign_sgd_apply(float *param, const uint64_t *vote_planes, int64_t P, flo
 typedef struct dls_qtile {
     int64_t dst;     /* first output element (flat layout offset, multiple of 16) */
     int64_t src;     /* first element within a client row of Q (kind 1/2) or F (kind 0) */
-    int32_t len;     /* elements: <= 4096 for the fast tiles, <= 1024 for the rest;
+    int32_t len;     /* elements: <= 4096 for the grouped tiles, <= 1024 for the rest;
                         lanes cover 16-element chunks (lane l, KiB slice g: element
                         1024 g + 16 l) up to the next multiple of 64 (the rows are
                         padded to 64) and write 0 past len, so the output's row
@@ -183,10 +183,13 @@ typedef struct dls_qtile {
  * bit-exact in client order.  Q int8/uint8 [*, ldq], F fp32 [*, ldf],
  * sz fp32 pairs (fl32(scale), zero_point): client row r, channel c at pair
  * r * sz_row + c * sz_chan (the store keeps them channel-major: sz_row = 1).
- * nfast: host array of 4 counts; the table starts with nfast[0] one-channel int
- * tiles of 4 KiB slices (3072 < len <= 4096), then nfast[1] of 3, nfast[2] of 2
- * and nfast[3] of 1 (len <= 1024); the remaining tiles (len <= 1024) may be of
- * any kind (see dls_qtile). */
+ * nfast: host array of DLS_QTILE_GROUPS counts; the table starts with
+ * nfast[0..3] one-channel int tiles of 4, 3, 2, 1 KiB slices (every real
+ * element in channel chan0), then nfast[4..7] multi-channel int tiles of 4, 3,
+ * 2, 1 KiB slices (channel rows a multiple of 16 elements: no lane's 16-element
+ * chunk straddles two channels), then nfast[8] fp32 tiles of <= 256 elements;
+ * the remaining tiles (len <= 1024) are int tiles of any shape (see dls_qtile). */
+#define DLS_QTILE_GROUPS 9
 int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast, const void *Q,
                        int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t sz_row,
                        int64_t sz_chan, const int32_t *rows, const float *weight, int32_t K,

@@ -360,3 +360,48 @@ def test_segment_minmax_ignores_nan():
         part = part[~torch.isnan(part)]
         assert float(mins[s]) == float(part.min()) and float(maxs[s]) == float(part.max()), s
     assert float(mins[-1]) == float("inf") and float(maxs[-1]) == float("-inf")
+
+
+@pytest.mark.parametrize("K", [1, 70])
+def test_dequant_fedavg_lane_tiles_resnet_shapes(K):
+    """Multi-channel (lane) tiles: ResNet-like conv / fc weights whose channel rows
+    are multiples of 16 (576, 1152, 32, 512), int8 symmetric and uint8 with zero
+    points, K across the 64-client chunk, one client with a scale beyond the
+    fast-division range (the per-client fallback); bit-exact vs the oracle."""
+    from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
+    g = torch.Generator().manual_seed(K + 17)
+    shapes = {"conv1": (5, 3, 3, 3), "l1": (8, 64, 3, 3), "l2": (4, 128, 3, 3),
+              "sc": (3, 32, 1, 1), "fc": (10, 512)}
+    payloads, n = [], []
+    for k in range(K):
+        p = {}
+        for name, s in shapes.items():
+            C = s[0]
+            if name == "l2":  # uint8 with zero points
+                p[name] = (torch.randint(0, 256, s, generator=g, dtype=torch.uint8),
+                           torch.rand(C, generator=g, dtype=torch.float64) * 1e-3 + 1e-5,
+                           torch.randint(0, 256, (C,), generator=g))
+            else:
+                sc = torch.rand(C, generator=g, dtype=torch.float64) * 1e-2 + 1e-4
+                if k == K // 2 and name == "l1":
+                    sc[2] = 3e30  # this client takes the fallback
+                p[name] = (torch.randint(-128, 128, s, generator=g, dtype=torch.int8), sc,
+                           torch.zeros(C, dtype=torch.int64))
+            p[name + ".bias"] = torch.randn(C, generator=g)
+        payloads.append(p)
+        n.append(int(torch.randint(1, 1000, (1,), generator=g)))
+    store = QuantizedClientStore(payloads[0], dev, capacity=K)
+    assert sum(store.nfast[4:]) > 0  # lane tiles are used
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    order = list(torch.randperm(K, generator=g).tolist())
+    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order]))
+    layout = [(k, tuple(v[0].shape) if isinstance(v, tuple) else tuple(v.shape))
+              for k, v in payloads[0].items()]
+    clients = [{k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy())
+                for k, v in p.items()} for p in payloads]
+    ref = oquant.dequant_fedavg(clients, n, order, layout)
+    assert same_bits(flat(out, layout), ref)

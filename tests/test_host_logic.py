@@ -50,11 +50,11 @@ def test_quant_layout_tiles():
     # one-channel int tiles first: the 15 tiles of the 3x5000 "u" are one-channel
     # except those starting at 4096 and 9216, which cross a row boundary
     nf = sum(nfast)
-    fast, rest = t[:nf], t[nf:]
+    fast, f32, rest = t[:nf - nfast[8]], t[nf - nfast[8]:nf], t[nf:]
     assert all(r["kind"] != 0 and r["row_pos"] + r["len"] <= r["row_len"] for r in fast)
-    assert all(r["kind"] == 0 or r["row_pos"] + r["len"] > r["row_len"] for r in rest)
-    assert sorted(rest["kind"].tolist()) == [0, 1, 2, 2]
-    assert nfast == (0, 0, 0, 13) and sum(int(r["len"]) for r in t) == 45 + 5 + 15000
+    assert all(r["row_pos"] + r["len"] > r["row_len"] for r in rest)
+    assert f32["kind"].tolist() == [0] and sorted(rest["kind"].tolist()) == [1, 2, 2]
+    assert nfast == (0, 0, 0, 13, 0, 0, 0, 0, 1) and sum(int(r["len"]) for r in t) == 45 + 5 + 15000
     u = t[t["kind"] == 2]
     assert all(int(r["row_pos"]) == int(r["src"] - ql.src[2]) % 5000 for r in u)
     assert all(int(r["chan0"]) == 5 + int(r["src"] - ql.src[2]) // 5000 for r in u)
@@ -63,20 +63,28 @@ def test_quant_layout_tiles():
 
 def test_quant_layout_channel_aligned_tiles():
     """Long channel rows (multiple of 64, last 1 KiB slice at least 7/8 full) get
-    channel-aligned tiles of up to 4096 elements, grouped by slice count."""
-    from distributed_learning_simulator_amd.quant_store import QuantLayout
-    shapes = {"fc": (3, 25088), "conv": (2, 512, 3, 3), "mid": (4, 256, 3, 3), "k": (2, 1024)}
+    channel-aligned tiles of up to 4096 elements, grouped by slice count; other
+    int tensors with rows a multiple of 16 get multi-channel (lane) tiles of
+    LANE_TILE elements from their start."""
+    from distributed_learning_simulator_amd.quant_store import LANE_TILE, QuantLayout
+    shapes = {"fc": (3, 25088), "conv": (2, 512, 3, 3), "mid": (4, 256, 3, 3), "k": (2, 1024),
+              "c1": (5, 3, 3, 3)}
     payload = {k: (torch.zeros(s, dtype=torch.int8), torch.ones(s[0]), torch.zeros(s[0]))
                for k, s in shapes.items()}
     ql = QuantLayout(payload)
     t, nfast = ql.tiles()
-    # fc: 6 x 4096 + 512 per channel; conv (row 4608): 4096 + 512; k: 1024;
-    # mid (row 2304: 768 idle lanes in its last slice) keeps 1 KiB tiles from its start
-    assert nfast == (3 * 6 + 2, 0, 0, 3 + 2 + 2 + 6)  # 6 of mid's 9 tiles lie in one channel
+    # fc: 6 x 4096 + 512 per channel (2 % idle lanes); k: 1024; conv (row 4608:
+    # 11 % idle lanes in its last slice) and mid (row 2304): lane tiles of
+    # LANE_TILE from their start; c1 (row 27): general 1 KiB tiles
+    assert LANE_TILE == 1024
+    assert nfast == (3 * 6, 0, 0, 3 + 2, 0, 0, 0, 9 + 9, 0)
     nf = sum(nfast)
-    sl = [(int(r["len"]) + 1023) // 1024 for r in t[:nf]]
+    one = t[:sum(nfast[:4])]
+    sl = [(int(r["len"]) + 1023) // 1024 for r in one]
     assert sl == sorted(sl, reverse=True)
-    assert all(r["row_pos"] + r["len"] <= r["row_len"] for r in t[:nf])
+    assert all(r["row_pos"] + r["len"] <= r["row_len"] for r in one)
+    lanes = t[sum(nfast[:4]):nf]
+    assert all(int(r["row_len"]) % 16 == 0 and int(r["len"]) <= LANE_TILE for r in lanes)
     assert all(d % 16 == 0 for d in t["dst"]) and all(s % 16 == 0 for s in t["src"])
     assert t["len"][nf:].max() <= 1024
     for i, name in enumerate(ql.names):  # every element of every tensor exactly once
@@ -88,6 +96,7 @@ def test_quant_layout_channel_aligned_tiles():
             cover[e:e + int(r["len"])] += 1
             assert int(r["src"]) - ql.src[i] == e
             assert int(r["chan0"]) == ql.chan_base[i] + e // ql.row_len[i]
+            assert int(r["row_pos"]) == e % ql.row_len[i]
         assert (cover == 1).all(), name
 
 

@@ -40,7 +40,7 @@ def test_python_binding_matches_header():
 
 def test_abi_version_and_error_without_gpu(lib):
     lib.dls_abi_version.restype = ctypes.c_int
-    assert lib.dls_abi_version() == 1
+    assert lib.dls_abi_version() == 2
     lib.dls_last_error.restype = ctypes.c_char_p
     # argument validation happens before any device call
     lib.dls_fedavg_f32.restype = ctypes.c_int

@@ -43,7 +43,7 @@ def load(path):
 
 
 def nfast_arg(L, counts):
-    return int(sum(counts)) if L.old_nfast else (ctypes.c_int32 * 4)(*counts)
+    return int(sum(counts)) if L.old_nfast else (ctypes.c_int32 * len(counts))(*counts)
 
 
 def ptr(t):
@@ -88,7 +88,7 @@ def setup(dev, want=()):
         pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
         W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
                      16 * (P * 4 + Wd * 8))
-    if {"quant", "quant1k", "quant_samerow"} & set(want):
+    if {"quant", "quant1k", "quant_samerow", "quant_w0", "quant_w8", "quant_w16"} & set(want):
         from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
         template = {}
         for name, s in vgg16():
@@ -126,6 +126,18 @@ def setup(dev, want=()):
                                                        tot, ptr(qo), stream()),
                         100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
         rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
+        from distributed_learning_simulator_amd import quant_store as qs0
+        for fwv in (0, 8, 16):
+            fw0, qs0.FAST_WASTE = qs0.FAST_WASTE, fwv
+            tvw, nfvw = st.qlayout.tiles()
+            qs0.FAST_WASTE = fw0
+            tvwd = torch.from_numpy(tvw.view(np.uint8).copy()).to(dev)
+            W[f"quant_w{fwv}"] = (
+                lambda L, tvwd=tvwd, tvw=tvw, nfvw=nfvw: L.dls_dequant_fedavg(
+                    ptr(tvwd), len(tvw), nfast_arg(L, nfvw), ptr(st.Q), st.Q.stride(0), ptr(st.F),
+                    st.F.stride(0), ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2,
+                    ptr(rows), ptr(w), 100, tot, ptr(qo), stream()),
+                100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
         W["quant_samerow"] = (lambda L: L.dls_dequant_fedavg(ptr(st.tiles), st.ntiles, nfast_arg(L, st.nfast),
                                                              ptr(st.Q), st.Q.stride(0),
                                                              ptr(st.F), st.F.stride(0), ptr(st.sz),
@@ -133,6 +145,44 @@ def setup(dev, want=()):
                                                              st.sz.stride(0) // 2, ptr(rows0), ptr(w),
                                                              100, tot, ptr(qo), stream()),
                               100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+    if any(w.startswith("quant_r18") for w in want):
+        # north-star: 1000 ResNet-18 int8 updates; quant_r18_l<N>: lane tiles of N KiB
+        from distributed_learning_simulator_amd import quant_store as qs
+        from distributed_learning_simulator_amd.quant_store import QuantizedClientStore as QCS
+        template = {}
+        for name, s in resnet18_cifar():
+            if len(s) >= 2:
+                template[name] = (torch.zeros(s, dtype=torch.int8), torch.ones(s[0], dtype=torch.float64),
+                                  torch.zeros(s[0], dtype=torch.int64))
+            else:
+                template[name] = torch.zeros(s)
+        sr = QCS(template, dev, capacity=1000)
+        sr.Q.random_(0, 256, generator=g)
+        sr.F.normal_(generator=g)
+        sr.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
+        sr.sz[..., 1].zero_()
+        r1k = torch.arange(1000, dtype=torch.int32, device=dev)
+        w1k = torch.randint(100, 1000, (1000,), generator=g, device=dev).float()
+        t1k = float(w1k.sum())
+        qo18 = torch.empty(sr.layout.P, device=dev)
+        qlr = sr.qlayout
+        nb = 1000 * (sum(m for m, k in zip(sr.layout.numels, qlr.kinds) if k) +
+                     4 * sum(m for m, k in zip(sr.layout.numels, qlr.kinds) if not k) + 8 * qlr.C) \
+            + 4 * sr.layout.numel
+        saved = qs.LANE_TILE
+        for lt, fwv in ((1, None), (2, None), (4, None), (1, 0), (1, 8), (1, 16)):
+            qs.LANE_TILE = 1024 * lt
+            fw, qs.FAST_WASTE = qs.FAST_WASTE, (qs.FAST_WASTE if fwv is None else fwv)
+            tt, nft = qlr.tiles()
+            qs.FAST_WASTE = fw
+            tdev = torch.from_numpy(tt.view(np.uint8).copy()).to(dev)
+            W[f"quant_r18_l{lt}" + (f"_w{fwv}" if fwv is not None else "")] = (
+                lambda L, tdev=tdev, tt=tt, nft=nft: L.dls_dequant_fedavg(
+                    ptr(tdev), len(tt), nfast_arg(L, nft), ptr(sr.Q), sr.Q.stride(0), ptr(sr.F),
+                    sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
+                    ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb)
+        qs.LANE_TILE = saved
+        W["quant_r18"] = W[f"quant_r18_l{saved // 1024}"]
     # Shapley default path: 50 coalitions (members with p = 1/2) over 50 clients,
     # each client row read once per batch (dls_subset_fedavg_union_f32)
     from distributed_learning_simulator_amd.aggregation import union_batch
