@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("DLS_HIP_LIB", os.path.join(_HERE, "libdls_hip.so"))
 FEDAVG_EXACT = 0
 FEDAVG_FMA = 1
 SIGN_NAN_MARK = 1 << 24
-QTILE_GROUPS = 9  # DLS_QTILE_GROUPS
+QTILE_GROUPS = 10  # DLS_QTILE_GROUPS
 SUBSET_UNION_MAX = 64  # DLS_SUBSET_UNION_MAX: coalitions per dls_subset_fedavg_union_f32 call
 
 

@@ -23,6 +23,10 @@ constexpr int kQuantSched = 2;  // element pairs between scheduling barriers
 #define DLS_LANE_U 2
 #endif
 constexpr int kLaneU = DLS_LANE_U;  // clients per batch on lane-channel tiles
+#ifndef DLS_LANE_SCHED
+#define DLS_LANE_SCHED 2
+#endif
+constexpr int kLaneSched = DLS_LANE_SCHED;  // element pairs between scheduling barriers
 
 __device__ __forceinline__ float byte_f32(uint32_t w, int k) {
     return (float)((w >> (8 * k)) & 0xffu);  // selects v_cvt_f32_ubyte{k}
@@ -126,7 +130,7 @@ __device__ __forceinline__ float byte_val(uint32_t w, int k) {
 // TWO: the two-constant division q = fma(t, yh, RN(t*yl)) (dls_common.h), valid
 // for this divisor when the host's exhaustive check passed (d.two): 2 packed ops
 // per element pair instead of Markstein's 3.
-template <bool ZFMA, bool FAST, bool SEXT = false, bool TWO = false>
+template <bool ZFMA, bool FAST, bool SEXT = false, bool TWO = false, int SCHED = kQuantSched>
 __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s, float zs, float z,
                                             float wk, const FastDiv &d) {
     const f32x2 s2 = f32x2{s, s}, w2 = f32x2{wk, wk};
@@ -152,7 +156,7 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
         acc[j + 1] = r.y;
         // keep the scheduler from widening the chain over all 16 elements of
         // every in-flight client (that costs ~60 VGPRs and waves per SIMD)
-        if ((j / 2) % kQuantSched == kQuantSched - 1) __builtin_amdgcn_sched_barrier(0);
+        if (SCHED > 0 && (j / 2) % SCHED == SCHED - 1) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -283,7 +287,8 @@ __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_
         f32x2 a, b;
         float wk;
     };
-    constexpr int U = 4;  // clients per batch, double-buffered (a latency chain otherwise)
+    constexpr int U = 8;  // clients per batch, double-buffered: a few waves walk all K clients, so
+                          // the loads of 2U clients in flight set the time (a latency chain)
     struct Batch {
         One c[U];
     };
@@ -302,13 +307,26 @@ __device__ __forceinline__ void int_lane_channels(float (&acc)[16], const uint8_
             if (SIGNED) o.qv ^= 0x80808080u;
             const float za = o.a.y + zadj, zb = o.b.y + zadj;
             const bool fast = d.fast && scale_fast(o.a.x * o.wk) && scale_fast(o.b.x * o.wk);
+            // wave-uniform: the common client carries Markstein only (a per-lane
+            // select would compute both divisions for every element)
+            if (__builtin_expect(__ballot(!fast) == 0, 1)) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const bool second = e >= split;
-                const float s = second ? o.b.x : o.a.x;
-                const float z = second ? zb : za;
-                const float t = ((byte_f32(o.qv[e >> 2], e & 3) - z) * s) * o.wk;
-                acc[e] += fast ? markstein(t, d.b, d.y) : t / d.b;
+                for (int e = 0; e < 16; ++e) {
+                    const bool second = e >= split;
+                    const float s = second ? o.b.x : o.a.x;
+                    const float z = second ? zb : za;
+                    const float t = ((byte_f32(o.qv[e >> 2], e & 3) - z) * s) * o.wk;
+                    acc[e] += markstein(t, d.b, d.y);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const bool second = e >= split;
+                    const float s = second ? o.b.x : o.a.x;
+                    const float z = second ? zb : za;
+                    const float t = ((byte_f32(o.qv[e >> 2], e & 3) - z) * s) * o.wk;
+                    acc[e] += fast ? markstein(t, d.b, d.y) : t / d.b;
+                }
             }
         };
         chunk_pipeline<U, Batch>(
@@ -566,8 +584,8 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
             if (__builtin_expect(__ballot(!ok) == 0, 1)) {
 #pragma unroll
                 for (int g = 0; g < G; ++g)
-                    accum16_one<true, true, SIGNED, TWO>(acc[g], b.qv[g], b.s[g].x,
-                                                         b.s[g].y * b.s[g].x, 0.f, b.wk, d);
+                    accum16_one<true, true, SIGNED, TWO, kLaneSched>(
+                        acc[g], b.qv[g], b.s[g].x, b.s[g].y * b.s[g].x, 0.f, b.wk, d);
             } else {  // rare clients: the reference's formula with IEEE division
 #pragma unroll
                 for (int g = 0; g < G; ++g)
@@ -642,7 +660,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_dequant_fast(
 // batches of kF32U clients double-buffered — so that the few waves of a small
 // tensor keep 2 * kF32U client rows in flight instead of one dependent load per
 // client (with K = 1000 clients the unpipelined loop is a ~2 ms latency chain).
-constexpr int kF32U = 8;
+constexpr int kF32U = 16;
 __global__ __launch_bounds__(kBlock) void k_dequant_f32(const dls_qtile *__restrict__ tiles,
                                                         int ntiles, const float *__restrict__ F,
                                                         int64_t ldf,
@@ -651,6 +669,9 @@ __global__ __launch_bounds__(kBlock) void k_dequant_f32(const dls_qtile *__restr
                                                         FastDiv d, float *__restrict__ out) {
     const int idx = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if (idx >= ntiles) return;  // wave-uniform
+    // a few waves that walk all K clients beside the bulk kernel's: without
+    // priority they get a fifth of their SIMD's issue slots and finish last
+    __builtin_amdgcn_s_setprio(3);
     const dls_qtile t = tiles[idx];
     const int e0 = 4 * __lane_id();
     const int lenpad = (t.len + 63) & ~63;
@@ -658,9 +679,18 @@ __global__ __launch_bounds__(kBlock) void k_dequant_f32(const dls_qtile *__restr
     const float *src = F + t.src + ec;
     f32x4 acc = f32x4{-0.f, -0.f, -0.f, -0.f};
     auto term = [&](f32x4 x, float wk) {
-        f32x4 q;
+        f32x4 t, q;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) q[c] = div_exact(x[c] * wk, d);
+        for (int c = 0; c < 4; ++c) t[c] = x[c] * wk;
+        const bool ok = d.fast && in_fast_range(t.x) && in_fast_range(t.y) && in_fast_range(t.z) &&
+                        in_fast_range(t.w);
+        if (__builtin_expect(__ballot(!ok) == 0, 1)) {  // wave-uniform common case
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q[c] = markstein(t[c], d.b, d.y);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q[c] = div_exact(t[c], d);
+        }
         return q;
     };
     struct Batch {
@@ -702,6 +732,101 @@ __global__ __launch_bounds__(kBlock) void k_dequant_f32(const dls_qtile *__restr
     }
 }
 
+// int tensors whose channel rows are not a multiple of 16 elements (the first
+// conv of a CIFAR ResNet: rows of 27): tiles of <= 256 elements, a lane owning 4
+// consecutive elements, which span at most two channels when rows are >= 4
+// long; the reference formula fl(fl(fl(q - zp) * s) * n) / N per element, the
+// pipelined client walk of k_dequant_f32.  Few waves, each a long client chain:
+// kept small so that it neither starves nor thrashes the instruction cache.
+template <bool SIGNED>
+__device__ __forceinline__ float small_byte(uint32_t w, int k) {
+    return SIGNED ? (float)(int8_t)(w >> (8 * k)) : (float)((w >> (8 * k)) & 0xffu);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dequant_small(const dls_qtile *__restrict__ tiles,
+                                                          int ntiles, const uint8_t *__restrict__ Q,
+                                                          int64_t ldq, const f32x2 *__restrict__ sz,
+                                                          SzLayout L,
+                                                          const int32_t *__restrict__ rows,
+                                                          const float *__restrict__ w, int K,
+                                                          FastDiv d, float *__restrict__ out) {
+    const int idx = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (idx >= ntiles) return;  // wave-uniform
+    __builtin_amdgcn_s_setprio(3);  // few long waves beside the bulk kernel's (cf. k_dequant_f32)
+    const dls_qtile t = tiles[idx];
+    const bool sgn = t.kind == 1;
+    const int e0 = 4 * __lane_id();
+    const int lenpad = (t.len + 3) & ~3;
+    const int ec = e0 < lenpad ? e0 : lenpad - 4;  // idle lanes load a valid duplicate
+    const int p = t.row_pos + ec;
+    const int c = min(t.chan0 + p / t.row_len, t.chan_end - 1);
+    const int split = t.row_len - p % t.row_len;  // elements of this lane in channel c
+    const int64_t ca = (int64_t)c * L.chan;
+    const int64_t cb = (int64_t)min(c + 1, t.chan_end - 1) * L.chan;
+    const uint8_t *src = Q + t.src + ec;
+    f32x4 acc = f32x4{-0.f, -0.f, -0.f, -0.f};
+    struct One {
+        uint32_t q;
+        f32x2 a, b;
+        float wk;
+    };
+    constexpr int U = 8;
+    struct Batch {
+        One c[U];
+    };
+    auto step = [&](const One &o) {
+        const bool fast = d.fast && scale_fast(o.a.x * o.wk) && scale_fast(o.b.x * o.wk);
+        f32x4 tt;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const bool second = e >= split;
+            const float x = sgn ? small_byte<true>(o.q, e) : small_byte<false>(o.q, e);
+            tt[e] = ((x - (second ? o.b.y : o.a.y)) * (second ? o.b.x : o.a.x)) * o.wk;
+        }
+        if (__builtin_expect(__ballot(!fast) == 0, 1)) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] += markstein(tt[e], d.b, d.y);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[e] += fast ? markstein(tt[e], d.b, d.y) : tt[e] / d.b;
+        }
+    };
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        cr.advance(rows, w, K, base);
+        auto fetch = [&](int j, One &o) {
+            const int64_t r = readlane_i(tr, j);
+            o.q = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(src + r * ldq));
+            o.a = sz[ca + r * L.row];
+            o.b = sz[cb + r * L.row];
+            o.wk = readlane_f(tw, j);
+        };
+        chunk_pipeline<U, Batch>(
+            min(64, K - base),
+            [&](int j0, Batch &b) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) fetch(j0 + u, b.c[u]);
+            },
+            [&](const Batch &b) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) step(b.c[u]);
+            },
+            [&](int j) {
+                One o;
+                fetch(j, o);
+                step(o);
+            });
+    }
+    if (e0 < lenpad) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = e0 + e < t.len ? acc[e] : 0.f;  // keep padding zero
+        *reinterpret_cast<f32x4 *>(out + t.dst + e0) = acc;
+    }
+}
+
 template <int G, bool TWO>
 __global__ __launch_bounds__(kBlock, 1) void k_dequant_lanes(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
@@ -722,6 +847,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_general(
     float *__restrict__ out) {
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
+    __builtin_amdgcn_s_setprio(3);  // few long waves beside the bulk kernel's (cf. k_dequant_f32)
     const dls_qtile &t = wt.t;
     float acc[16];
 #pragma unroll
@@ -961,7 +1087,7 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
     // Groups: 0-3 one-channel tiles of 4/3/2/1 KiB slices, 4-7 lane-channel tiles
-    // of 4/3/2/1 slices, 8 fp32 tiles, then the general tiles.  The group with
+    // of 4/3/2/1 slices, 8 fp32 tiles, 9 small int tiles, then the general tiles.  The group with
     // the most bytes runs on the caller's stream; every other non-empty group on a
     // side stream of its own, concurrently (their waves walk all K clients, so a
     // small group is a long latency chain, not a small amount of work), and the
@@ -970,7 +1096,7 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     const dls_qtile *t = tiles;
     int big = -1;
     auto bytes = [&](int g) {  // ~ bytes per client of group g
-        return g < 8 ? (int64_t)nfast[g] * 1024 * (4 - g % 4) : (int64_t)nfast[g] * 1024;
+        return g < 8 ? (int64_t)nfast[g] * 1024 * (4 - g % 4) : (int64_t)nfast[g] * 256;
     };
     for (int g = 0; g < DLS_QTILE_GROUPS; ++g) {
         tg[g] = t;
@@ -1019,6 +1145,13 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
         if (g == 8) {
             hipLaunchKernelGGL(k_dequant_f32, dim3((unsigned)((n + wpb - 1) / wpb)), dim3(kBlock),
                                0, s, tg[g], n, F, ldf, rows, weight, (int)K, d, out);
+            return;
+        }
+        if (g == 9) {
+            hipLaunchKernelGGL(k_dequant_small, dim3((unsigned)((n + wpb - 1) / wpb)),
+                               dim3(kBlock), 0, s, tg[g], n, reinterpret_cast<const uint8_t *>(Q),
+                               ldq, reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d,
+                               out);
             return;
         }
         const Kfn kern = kgroup[g][d.two ? 1 : 0];

@@ -112,9 +112,11 @@ class QuantLayout:
           channels: 3x3 convs, fc layers) are cut into LANE_TILE-element tiles from
           their start, each lane loading its own channel's (scale, zp);
         * fp32 tiles (group 8, <= F32_TILE elements): the fp32 tensors;
-        * general tiles (<= TILE elements): the remaining int tensors (rows
-          shorter than 16 or not a multiple of 16)."""
-        rows, lane_rows, f32_rows = [], [], []
+        * small int tiles (group 9, <= F32_TILE elements): the other int tensors
+          with rows of at least 4 elements (a lane's 4 span <= 2 channels), except
+          their 1 KiB pieces that lie inside one channel (one-channel group 3);
+        * general tiles (<= TILE elements): int tensors with rows shorter than 4."""
+        rows, lane_rows, f32_rows, small_rows = [], [], [], []
         for i, kind in enumerate(self.kinds):
             n = self.layout.numels[i]
             rl = self.row_len[i]
@@ -138,6 +140,18 @@ class QuantLayout:
                 for e in range(0, n, F32_TILE):
                     f32_rows.append((off + e, src + e, min(F32_TILE, n - e), 0, 0, 1, 0, 0))
                 continue
+            if rl >= 4:
+                # 1 KiB tiles from the tensor start; those inside one channel run on
+                # the one-channel kernel, the others are cut into small tiles
+                for e in range(0, n, TILE):
+                    ln = min(TILE, n - e)
+                    if e % rl + ln <= rl:
+                        rows.append((off + e, src + e, ln, kind, cb + e // rl, rl, e % rl, cend))
+                        continue
+                    for e2 in range(e, e + ln, F32_TILE):
+                        small_rows.append((off + e2, src + e2, min(F32_TILE, e + ln - e2), kind,
+                                           cb + e2 // rl, rl, e2 % rl, cend))
+                continue
             for e in range(0, n, TILE):
                 rows.append((off + e, src + e, min(TILE, n - e), kind, cb + e // rl if kind else 0,
                              rl, e % rl if kind else 0, cend))
@@ -150,7 +164,7 @@ class QuantLayout:
 
         fast = [[r for r in rows if one_channel(r) and slices(r) == g] for g in (4, 3, 2, 1)]
         fast += [[r for r in lane_rows if slices(r) == g] for g in (4, 3, 2, 1)]
-        fast += [f32_rows]
+        fast += [f32_rows, small_rows]
         rest = [r for r in rows if not one_channel(r)]
         assert all(r[2] <= TILE for r in rest)
         return (np.array([r for grp in fast for r in grp] + rest, dtype=QTILE_DTYPE),

@@ -187,9 +187,11 @@ typedef struct dls_qtile {
  * nfast[0..3] one-channel int tiles of 4, 3, 2, 1 KiB slices (every real
  * element in channel chan0), then nfast[4..7] multi-channel int tiles of 4, 3,
  * 2, 1 KiB slices (channel rows a multiple of 16 elements: no lane's 16-element
- * chunk straddles two channels), then nfast[8] fp32 tiles of <= 256 elements;
- * the remaining tiles (len <= 1024) are int tiles of any shape (see dls_qtile). */
-#define DLS_QTILE_GROUPS 9
+ * chunk straddles two channels), then nfast[8] fp32 tiles of <= 256 elements,
+ * nfast[9] int tiles of <= 256 elements of tensors with channel rows of >= 4
+ * elements (a lane's 4 elements span at most two channels); the remaining tiles
+ * (len <= 1024) are int tiles of any shape (see dls_qtile). */
+#define DLS_QTILE_GROUPS 10
 int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast, const void *Q,
                        int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t sz_row,
                        int64_t sz_chan, const int32_t *rows, const float *weight, int32_t K,

@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/trace" -o run -- \
     python3 "$ROOT/tools/ab_bench.py" --workloads "$WL" --only-run --launches 10 > "$OUT/trace.log" 2>&1 || exit $?
-cp "$RAW/trace/run_kernel_stats.csv" "$OUT/" 2>/dev/null
+cp "$RAW/trace/run_kernel_stats.csv" "$OUT/" 2>/dev/null; grep -E "dls::|Kernel_Name" "$RAW/trace/run_kernel_trace.csv" > "$OUT/kernel_trace_dls.csv" 2>/dev/null
 i=0
 for G in "$@"; do
     i=$((i + 1))

@@ -43,18 +43,23 @@ def test_quant_layout_tiles():
     from distributed_learning_simulator_amd.quant_store import QuantLayout
     payload = {"w": (torch.zeros(5, 9, dtype=torch.int8), torch.ones(5), torch.zeros(5)),
                "b": torch.zeros(5),
-               "u": (torch.zeros(3, 5000, dtype=torch.uint8), torch.ones(3), torch.zeros(3))}
+               "u": (torch.zeros(3, 5000, dtype=torch.uint8), torch.ones(3), torch.zeros(3)),
+               "v": (torch.zeros(6, 3, dtype=torch.int8), torch.ones(6), torch.zeros(6))}
     ql = QuantLayout(payload)
     t, nfast = ql.tiles()
     assert t["len"].max() <= 1024 and all(d % 16 == 0 for d in t["dst"])
-    # one-channel int tiles first: the 15 tiles of the 3x5000 "u" are one-channel
-    # except those starting at 4096 and 9216, which cross a row boundary
-    nf = sum(nfast)
-    fast, f32, rest = t[:nf - nfast[8]], t[nf - nfast[8]:nf], t[nf:]
-    assert all(r["kind"] != 0 and r["row_pos"] + r["len"] <= r["row_len"] for r in fast)
-    assert all(r["row_pos"] + r["len"] > r["row_len"] for r in rest)
-    assert f32["kind"].tolist() == [0] and sorted(rest["kind"].tolist()) == [1, 2, 2]
-    assert nfast == (0, 0, 0, 13, 0, 0, 0, 0, 1) and sum(int(r["len"]) for r in t) == 45 + 5 + 15000
+    # the 15 1 KiB tiles of the 3x5000 "u" lie in one channel except those starting
+    # at 4096 and 9216 (cut into small tiles); "w" (rows of 9): one small tile;
+    # "b": one fp32 tile; "v" (rows of 3): a general tile
+    g = np.cumsum((0,) + nfast)
+    one = t[:g[4]]
+    assert all(r["kind"] != 0 and r["row_pos"] + r["len"] <= r["row_len"] for r in one)
+    assert t[g[8]:g[9]]["kind"].tolist() == [0]
+    small, rest = t[g[9]:g[10]], t[g[10]:]
+    assert all(int(r["len"]) <= 256 and int(r["row_len"]) >= 4 for r in small)
+    assert rest["kind"].tolist() == [1] and int(rest[0]["row_len"]) == 3
+    assert nfast == (0, 0, 0, 13, 0, 0, 0, 0, 1, 1 + 4 + 4)
+    assert sum(int(r["len"]) for r in t) == 45 + 5 + 15000 + 18
     u = t[t["kind"] == 2]
     assert all(int(r["row_pos"]) == int(r["src"] - ql.src[2]) % 5000 for r in u)
     assert all(int(r["chan0"]) == 5 + int(r["src"] - ql.src[2]) // 5000 for r in u)
@@ -77,16 +82,17 @@ def test_quant_layout_channel_aligned_tiles():
     # 11 % idle lanes in its last slice) and mid (row 2304): lane tiles of
     # LANE_TILE from their start; c1 (row 27): general 1 KiB tiles
     assert LANE_TILE == 1024
-    assert nfast == (3 * 6, 0, 0, 3 + 2, 0, 0, 0, 9 + 9, 0)
+    assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 0, 0, 0, 9 + 9) and nfast[8] == 0
+    assert nfast[9] == (5 * 27 + 255) // 256  # c1 (rows of 27): small tiles
     nf = sum(nfast)
     one = t[:sum(nfast[:4])]
     sl = [(int(r["len"]) + 1023) // 1024 for r in one]
     assert sl == sorted(sl, reverse=True)
     assert all(r["row_pos"] + r["len"] <= r["row_len"] for r in one)
-    lanes = t[sum(nfast[:4]):nf]
+    lanes = t[sum(nfast[:4]):sum(nfast[:8])]
     assert all(int(r["row_len"]) % 16 == 0 and int(r["len"]) <= LANE_TILE for r in lanes)
     assert all(d % 16 == 0 for d in t["dst"]) and all(s % 16 == 0 for s in t["src"])
-    assert t["len"][nf:].max() <= 1024
+    assert nf == len(t)  # no general tiles
     for i, name in enumerate(ql.names):  # every element of every tensor exactly once
         mine = t[(t["dst"] >= ql.layout.offsets[i]) &
                  (t["dst"] < ql.layout.offsets[i] + ql.layout.numels[i])]
