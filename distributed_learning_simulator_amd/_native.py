@@ -150,13 +150,15 @@ def subset_fedavg(U, sub_off, sub_rows, sub_weight, sub_total, P, out, stream=No
 
 def subset_fedavg_union(U, urows, uweight, member, sub_total, P, out, stream=None):
     """S <= SUBSET_UNION_MAX coalitions over one client union, each client row read
-    once (dls_subset_fedavg_union_f32); member: int64 [Ku] bit masks."""
+    once (dls_subset_fedavg_union_f32); member: int64 [Ku] bit masks (device);
+    sub_total: the S divisors fl32(N_s) (host: a sequence of numbers)."""
     assert urows.dtype == torch.int32 and uweight.dtype == torch.float32
-    assert member.dtype == torch.int64 and sub_total.dtype == torch.float32
-    S = sub_total.numel()
+    assert member.dtype == torch.int64
+    tot = [float(x) for x in sub_total]
+    S = len(tot)
     _check(lib().dls_subset_fedavg_union_f32(_ptr(U), U.stride(0), _ptr(urows), _ptr(uweight),
-                                             _ptr(member), urows.numel(), _ptr(sub_total), S, P,
-                                             _ptr(out), out.stride(0), _stream(stream, U)),
+                                             _ptr(member), urows.numel(), (ctypes.c_float * S)(*tot),
+                                             S, P, _ptr(out), out.stride(0), _stream(stream, U)),
            "dls_subset_fedavg_union_f32")
     return out
 

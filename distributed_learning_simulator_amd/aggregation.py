@@ -60,9 +60,9 @@ def union_order(subsets):
 
 
 def union_batch(subsets, n_of_row, device):
-    """Device tables of dls_subset_fedavg_union_f32 for <= 64 subsets (row lists)
-    over one union order: (urows int32, uweight fp32, member int64 masks,
-    sub_total fp32), or None when no common order exists."""
+    """Tables of dls_subset_fedavg_union_f32 for <= 64 subsets (row lists) over one
+    union order: (urows int32, uweight fp32, member int64 masks) on the device and
+    the divisors as a host list, or None when no common order exists."""
     order = union_order(subsets)
     if order is None:
         return None
@@ -74,8 +74,7 @@ def union_batch(subsets, n_of_row, device):
     member = [m - (1 << 64) if m >= 1 << 63 else m for m in member]  # as int64
     totals = [float(sum(int(n_of_row[r]) for r in sub)) for sub in subsets]
     return (_i32(order, device), _f32([int(n_of_row[r]) for r in order], device),
-            torch.tensor(member, dtype=torch.int64).to(device, non_blocking=True),
-            _f32(totals, device))
+            torch.tensor(member, dtype=torch.int64).to(device, non_blocking=True), totals)
 
 
 class ClientUpdateStore:
@@ -151,7 +150,7 @@ class ClientUpdateStore:
             if all(t is not None for t in tables):
                 for i, t in enumerate(tables):
                     c0 = i * _native.SUBSET_UNION_MAX
-                    _native.subset_fedavg_union(self.U, *t, P, out[c0:c0 + t[3].numel()])
+                    _native.subset_fedavg_union(self.U, *t, P, out[c0:c0 + len(t[3])])
                 return out
         if method == "exact":
             off, flat_rows, flat_w, totals = [0], [], [], []

@@ -83,6 +83,9 @@ inline FastDiv make_fastdiv(float b) {
 // Exhaustive check of the two-constant division for divisor b (every fp32
 // mantissa of a in [1,2)); thread-safe, memoised per b (~ms on first use).
 bool two_constant_exact(float b, float yh, float yl);
+// Run the checks of the not yet memoised divisors among b[0..n) in parallel
+// (host threads), so that make_fastdiv2 on each of them is then a cache hit.
+void prove_two_constant(const float *b, int n);
 
 inline FastDiv make_fastdiv2(float b) {
     FastDiv d = make_fastdiv(b);

@@ -6,7 +6,9 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
+#include <vector>
 
 #include "dls_common.h"
 
@@ -99,9 +101,12 @@ __attribute__((target("avx2,fma"))) static bool two_constant_block(uint32_t m0, 
     return bad == 0;
 }
 
+static std::mutex g_two_mu;
+static std::unordered_map<uint32_t, bool> g_two_cache;
+
 bool two_constant_exact(float b, float yh, float yl) {
-    static std::mutex mu;
-    static std::unordered_map<uint32_t, bool> cache;
+    std::mutex &mu = g_two_mu;
+    std::unordered_map<uint32_t, bool> &cache = g_two_cache;
     uint32_t key;
     memcpy(&key, &b, 4);
     {
@@ -114,6 +119,27 @@ bool two_constant_exact(float b, float yh, float yl) {
     std::lock_guard<std::mutex> g(mu);
     cache[key] = ok;
     return ok;
+}
+
+void prove_two_constant(const float *b, int n) {
+    std::vector<float> todo;
+    {
+        std::lock_guard<std::mutex> g(g_two_mu);
+        for (int i = 0; i < n; ++i) {
+            uint32_t key;
+            memcpy(&key, &b[i], 4);
+            const FastDiv d = make_fastdiv(b[i]);
+            if (d.fast && g_two_cache.find(key) == g_two_cache.end()) todo.push_back(b[i]);
+        }
+    }
+    if (todo.size() < 2) return;  // make_fastdiv2 does a single one itself
+    const int nt = (int)std::min<size_t>(todo.size(), std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < todo.size(); i += nt) (void)make_fastdiv2(todo[i]);
+        });
+    for (auto &x : th) x.join();
 }
 
 }  // namespace dls

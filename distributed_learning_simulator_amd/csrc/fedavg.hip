@@ -13,6 +13,8 @@
 //     term_i = fl(fl(x * fl32(n_i)) / fl32(N)); acc = term_0; acc = fl(acc + term_i)
 // (division: dls_common.h, Markstein fast path + IEEE fix-up for out-of-range).
 // FMA mode computes acc = fma(x, fl(n_i/N), acc) (normwise ~1e-7).
+#include <cstring>
+
 #include "dls_common.h"
 
 namespace dls {
@@ -251,17 +253,24 @@ constexpr int kUnionWaves = 8;   // waves per block: <= 8 clients staged, <= KW 
 // issues exactly KW stores and NL loads per tile: the compiler's vmcnt waits
 // are then exact, and waiting for the next tile's loads never waits for this
 // tile's younger stores).
+// Per-coalition division constants, computed on the host (dls_common.h FastDiv):
+// {yh = RN(1/N), yl = RN(1/N - yh), N, flags}; flags bit 0: the two-constant
+// quotient fma(t, yh, RN(t * yl)) is proven correctly rounded for this N (the
+// host's exhaustive mantissa check), bit 1: N in Markstein's range [1, 2^31].
+struct UnionDiv {
+    f32x4 c[DLS_SUBSET_UNION_MAX];
+};
+
 template <int KW, bool ACC>
 __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
     const f32x4 *__restrict__ Uv, int64_t ldu4, const int32_t *__restrict__ urows,
-    const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku,
-    const float *__restrict__ sub_total, int S, int64_t P4, int64_t ntiles,
-    f32x4 *__restrict__ out, int64_t ldo4) {
+    const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku, UnionDiv dv, int S,
+    int64_t P4, int64_t ntiles, f32x4 *__restrict__ out, int64_t ldo4) {
     constexpr int W = kUnionWaves, NL = kUnionChunk / kUnionWaves;
     // 69 KiB in all, so two blocks (16 waves) share a CU
     __shared__ f32x4 ts[kUnionChunk * 64];                    // 64 KiB: t_j of this tile
     __shared__ uint8_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk];  // member positions, per coalition
-    __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];               // {y, y, N, N} per coalition
+    __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];               // UnionDiv, per coalition
     __shared__ uint32_t tbad[W];                              // per loader wave: t out of range
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;  // block-uniform
@@ -292,12 +301,9 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
                     lst[c][__builtin_amdgcn_mbcnt_hi((uint32_t)(in >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)in, 0u))] =
                         (uint8_t)lane;
-                const float b = sub_total[c];
-                const float y = (float)(1.0 / (double)b);
-                if (lane == 0) cst[c] = f32x4{y, y, b, b};
+                if (lane == 0) cst[c] = dv.c[c];
             }
-            const float b = sub_total[c];
-            fast &= (int)(b >= 1.0f && b <= 2147483648.0f);
+            fast &= (int)((__float_as_uint(dv.c[c].w) & 2u) != 0);
         }
     }
     // loader slots: wave wv stages clients wv + W l, l < NL (past Ku: a duplicate
@@ -368,16 +374,26 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
                 f32x4 acc = acc_in[k];
                 if (__builtin_expect(tile_fast, 1)) {
                     const f32x4 cc = cst[c];
-                    const f32x2 y2 = f32x2{cc.x, cc.y}, b2 = f32x2{cc.z, cc.w};
+                    const f32x2 y2 = f32x2{cc.x, cc.x}, l2 = f32x2{cc.y, cc.y};
+                    const f32x2 b2 = f32x2{cc.z, cc.z};
+                    const bool two = (__float_as_uint(cc.w) & 1u) != 0;  // wave-uniform
                     const uint32_t vl = (uint32_t)lst[c][lane] << 10;  // lane l: member l's offset
                     const int n = len[k];
+                    // q = RN(t / N): two-constant (2 ops) when proven for N, else
+                    // Markstein (3 ops); element pairs in v_pk_* (the scalar roundings)
                     auto quot = [&](f32x4 t) {
                         const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
-                        const f32x2 ql0 = tl * y2, qh0 = th * y2;
-                        const f32x2 ql = __builtin_elementwise_fma(
-                            __builtin_elementwise_fma(-ql0, b2, tl), y2, ql0);
-                        const f32x2 qh = __builtin_elementwise_fma(
-                            __builtin_elementwise_fma(-qh0, b2, th), y2, qh0);
+                        f32x2 ql, qh;
+                        if (two) {
+                            ql = __builtin_elementwise_fma(tl, y2, tl * l2);
+                            qh = __builtin_elementwise_fma(th, y2, th * l2);
+                        } else {
+                            const f32x2 ql0 = tl * y2, qh0 = th * y2;
+                            ql = __builtin_elementwise_fma(__builtin_elementwise_fma(-ql0, b2, tl),
+                                                           y2, ql0);
+                            qh = __builtin_elementwise_fma(__builtin_elementwise_fma(-qh0, b2, th),
+                                                           y2, qh0);
+                        }
                         return f32x4{ql.x, ql.y, qh.x, qh.y};
                     };
                     auto tload = [&](int l) {
@@ -407,10 +423,11 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
                     }
                     for (; l < n; ++l) acc = add4(acc, quot(tload(l)));
                 } else {
+                    const f32x4 cc = cst[c];
                     FastDiv d;
-                    d.b = sub_total[c];
-                    d.y = (float)(1.0 / (double)d.b);
-                    d.fast = d.b >= 1.0f && d.b <= 2147483648.0f;
+                    d.b = cc.z;
+                    d.y = cc.x;
+                    d.fast = (__float_as_uint(cc.w) & 2u) != 0;
                     for (int j = 0; j < Ku; ++j) {
                         if (!__builtin_amdgcn_readlane((int)((mj >> c) & 1ull), j)) continue;
                         const f32x4 t = ts[j * 64 + lane];
@@ -531,6 +548,18 @@ extern "C" int dls_subset_fedavg_union_f32(const float *U, int64_t ldu, const in
     const int64_t P4 = P / 4;
     const int64_t ntiles = (P4 + 63) / 64;
     hipStream_t st = as_stream(stream);
+    // division constants per coalition (host array sub_total): the exhaustive
+    // two-constant checks of new divisors run in parallel, then cached
+    UnionDiv dv;
+    prove_two_constant(sub_total, S);
+    for (int c = 0; c < S; ++c) {
+        const FastDiv d = make_fastdiv2(sub_total[c]);
+        const uint32_t flags = (d.two ? 1u : 0u) | (d.fast ? 2u : 0u);
+        float f;
+        memcpy(&f, &flags, 4);
+        dv.c[c] = f32x4{d.y, d.yl, d.b, f};
+    }
+    for (int c = S; c < DLS_SUBSET_UNION_MAX; ++c) dv.c[c] = f32x4{1.f, 0.f, 1.f, 0.f};
     // unions of more than 64 clients: one launch per 64-client chunk, each
     // continuing the running sums in `out` (the same fp32 additions, in order)
     for (int32_t c0 = 0; c0 < Ku; c0 += kUnionChunk) {
@@ -541,7 +570,7 @@ extern "C" int dls_subset_fedavg_union_f32(const float *U, int64_t ldu, const in
             const dim3 grid((unsigned)(ntiles < blocks ? ntiles : blocks));
             hipLaunchKernelGGL(kern, grid, dim3(64 * kUnionWaves), 0, st,
                                reinterpret_cast<const f32x4 *>(U), ldu / 4, urows + c0,
-                               uweight + c0, member + c0, kc, sub_total, (int)S, P4, ntiles,
+                               uweight + c0, member + c0, kc, dv, (int)S, P4, ntiles,
                                reinterpret_cast<f32x4 *>(out), ldo / 4);
         };
         const int kw = (S + kUnionWaves - 1) / kUnionWaves;

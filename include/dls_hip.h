@@ -95,7 +95,9 @@ int dls_subset_fedavg_f32(const float *U, int64_t ldu, const int32_t *sub_off,
  *   urows   int32 [Ku]   row of U of each client of the batch's union
  *   uweight fp32  [Ku]   fl32(n_j)
  *   member  uint64 [Ku]  bit s set iff client j belongs to coalition s
- *   sub_total fp32 [S]   fl32(N_s) of coalition s; S <= DLS_SUBSET_UNION_MAX
+ *   sub_total fp32 [S]   fl32(N_s) of coalition s, a HOST array (the library
+ *                        derives each coalition's division constants on the
+ *                        host, cf. dls_two_constant_division); S <= DLS_SUBSET_UNION_MAX
  * Row s of out [S, ldo] is coalition s's weighted mean, its members summed in
  * union order: bit-exact with the reference when every coalition lists its
  * clients in the union's order (the caller orders the union so — sorted

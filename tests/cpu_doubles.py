@@ -46,7 +46,7 @@ def subset_fedavg_union(U, urows, uweight, member, sub_total, P, out, stream=Non
     rows = _f32(urows).astype(np.int64)
     w = _f32(uweight)
     m = _f32(member).view(np.uint64)
-    tot = _f32(sub_total)
+    tot = np.asarray([float(x) for x in sub_total], np.float32)
     for s in range(tot.size):
         sel = [j for j in range(rows.size) if (int(m[j]) >> s) & 1]
         fedavg(U, torch.from_numpy(rows[sel].astype(np.int32)),

@@ -180,8 +180,9 @@ def _union(Ud, n, subsets, P=None):
 def test_subset_union_bit_exact(S):
     """dls_subset_fedavg_union_f32 (every client row read once per batch) vs the
     reference op order, per coalition: rows in arbitrary order, > 64 clients
-    (two table chunks), a ragged last tile, and special values that send some
-    tiles down the redo path (zeros, denormals, huge, inf, nan)."""
+    (two chained launches), a ragged last tile, special values that send some
+    tiles down the slow path (zeros, denormals, huge, inf, nan), and both
+    division methods (a coalition total that fails the two-constant proof)."""
     K, P = 70, 4096 * 3 + 12
     g = torch.Generator().manual_seed(S)
     U = (torch.randn(K, P, generator=g) * 0.05).numpy()
@@ -196,6 +197,9 @@ def test_subset_union_bit_exact(S):
         members = sorted(torch.randperm(K, generator=g)[:k].tolist())
         subsets.append([perm[w] for w in members])
     subsets[0] = [perm[w] for w in range(K)]
+    if S > 1:  # a divisor for which the two-constant quotient is not exact: Markstein
+        n[5] = 11735695
+        subsets[1] = [perm[5]]
     got = _union(torch.from_numpy(U).to(dev), n, subsets).cpu().numpy()
     for s, sub in enumerate(subsets):
         assert same_bits(got[s], _c.fedavg_ref(U, n, sub)), s

@@ -263,7 +263,7 @@ def test_union_batch_tables():
     m = [int(x) & (2**64 - 1) for x in member.tolist()]
     assert m[0] == 0b101 and m[1] == 0b011 and m[2] == 0b110
     assert m[3] == (1 << 2) | sum(1 << s for s in range(3, 64))
-    assert tot.tolist()[:3] == [30.0, 40.0, 90.0]
+    assert list(tot)[:3] == [30.0, 40.0, 90.0]
 
 
 def test_subset_models_union_path_matches_reference_order(doubles):

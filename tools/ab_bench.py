@@ -194,8 +194,9 @@ def setup(dev, want=()):
     ur, uwt, um, ut = union_batch(subs, nrow, dev)
     uo = torch.empty((50, P), device=dev)
     pairs = int(member.sum())
+    uth = (ctypes.c_float * len(ut))(*ut)
     W["union"] = (lambda L: L.dls_subset_fedavg_union_f32(ptr(U), P, ptr(ur), ptr(uwt), ptr(um), 50,
-                                                          ptr(ut), 50, P, ptr(uo), P, stream()),
+                                                          uth, 50, P, ptr(uo), P, stream()),
                   100 * P * 4)
     off, fr, fw, ft = [0], [], [], []
     for sub in subs:
