@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise scripts_gpu_profile.sh output into profiles/.
+
+* profiles/pmc_traffic.json: HBM bytes per C-ABI call for each bench roofline
+  key (read by bench.py as roofline.traffic), from the FETCH_SIZE / WRITE_SIZE
+  passes: every pass makes exactly 3 calls (tools/ab_bench.py --only-run
+  --launches 3), so bytes per call = the sum over all of
+  this library's kernels in the pass / 4 (one call may launch several kernels:
+  FedAvg's one-generation pieces, fed_quant's tile groups).
+  Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are KiB; on
+  gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads,
+  so hbm_read = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B stores.
+* profiles/<tag>_pmc_summary.txt: the same plus the SQ counter ratios.
+
+    python tools/pmc_traffic.py <tag>
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CALLS = 3
+KEYS = {"fedavg": "headline", "fedavg1k": "fedavg_k1000", "vote_sign": "sign_vote",
+        "pack": "sign_pack", "quant": "fed_quant", "quant_r18": "fed_quant_k1000",
+        "union": "shapley_exact", "gemm": "shapley_gemm"}
+
+
+def sums(path):
+    tot = collections.defaultdict(float)
+    kernels = set()
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            tot[row["Counter_Name"]] += float(row["Counter_Value"])
+            m = re.search(r"(k_\w+(<[^>]*>)?)", row["Kernel_Name"])
+            kernels.add(m.group(1) if m else row["Kernel_Name"][:40])
+    return tot, sorted(kernels)
+
+
+def main(tag):
+    base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    out_json, lines = {}, [f"# rocprofv3 PMC passes, tag {tag}: per C-ABI call ({CALLS} calls per pass)"]
+    for wl, key in KEYS.items():
+        try:
+            f, kern = sums(os.path.join(base, f"pmc_{wl}_FETCH_SIZE", "run_counter_collection.csv"))
+            w, _ = sums(os.path.join(base, f"pmc_{wl}_WRITE_SIZE", "run_counter_collection.csv"))
+        except OSError:
+            continue
+        rd = 2 * f["FETCH_SIZE"] * 1024 / CALLS
+        wr = w["WRITE_SIZE"] * 1024 / CALLS
+        out_json[key] = {"kernels": kern, "fetch_size_kib": f["FETCH_SIZE"] / CALLS,
+                         "write_size_kib": w["WRITE_SIZE"] / CALLS, "hbm_read_bytes": rd,
+                         "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr, "calls": CALLS}
+        lines.append(f"{key:16s} read {rd / 1e9:8.4f} GB  write {wr / 1e9:8.4f} GB  "
+                     f"total {(rd + wr) / 1e9:8.4f} GB  kernels {', '.join(kern)}")
+        try:
+            sq, _ = sums(os.path.join(base, f"pmc_{wl}_SQ_WAVES", "run_counter_collection.csv"))
+            wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
+            lines.append("    SQ per call: " + ", ".join(f"{k}={v / CALLS:.4g}" for k, v in sorted(sq.items())))
+            lines.append("    of SQ_WAVE_CYCLES: " + ", ".join(
+                f"{k}={sq[k] / wc:.3f}" for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")
+                if k in sq))
+        except OSError:
+            pass
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fo:
+        json.dump(out_json, fo, indent=1)
+    with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.txt"), "w") as fo:
+        fo.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02")
