@@ -24,6 +24,7 @@ import logging
 import torch
 
 from .. import _native
+from ..model_util import get_data_serialization_size
 from ..quant_store import QuantizedClientStore
 from .fed_server import FedServer
 
@@ -72,8 +73,9 @@ class FedQuantServer(FedServer):
         _native.quantize_u8(flat, seg, layout.P, scale, zp, q, deq, stochastic=self.stochastic,
                             seed=self.seed + self.round)
         self.quantized_parameter = (q, scale, zp)
-        parameter_size = layout.numel * 4
-        quantized_parameter_size = layout.numel + T * 8
+        # serialized sizes, as the reference's call site (:41-42)
+        parameter_size = get_data_serialization_size(aggregated_parameter)
+        quantized_parameter_size = get_data_serialization_size(self.quantized_parameter)
         log.warning(
             "parameter_size is %s, quantized_parameter_size is %s, compression ratio is %s",
             parameter_size, quantized_parameter_size,

@@ -2,7 +2,7 @@
 
 The reference trains with the absent library's QAT, sends
 ``qat.get_quantized_parameters()`` to a ``self.server`` attribute that does not
-exist (D2, so it never runs), logs the pickle-size compression ratio and loads
+exist (D2, so it never runs), logs the pickle-size compression ratio (``model_util.get_data_serialization_size``) and loads
 the server's answer.  This worker keeps the evident protocol on the task
 queue: after each ``trainer.train()`` it quantizes every weight tensor (dim >= 2)
 per output channel, symmetric int8 — torch's default QAT weight scheme
@@ -16,7 +16,7 @@ import logging
 import torch
 
 from .. import _native
-from ..model_util import ModelUtil
+from ..model_util import ModelUtil, get_data_serialization_size
 from ..trainer import ModelExecutorCallbackPoint
 from .fed_worker import dataset_size
 from .worker import Worker
@@ -50,7 +50,9 @@ class FedQuantWorker(Worker):
         self.round = worker_round
         self.trainer.add_named_callback(ModelExecutorCallbackPoint.AFTER_EXECUTE, "quantization",
                                         self.__send_parameters)
-        self.parameter_size = sum(p.numel() * 4 for p in self.trainer.model.parameters())
+        # serialized sizes, as the reference (workers/fed_quant_worker.py:28-30,43)
+        self.parameter_size = get_data_serialization_size(
+            ModelUtil(self.trainer.model).get_parameter_dict())
         self.quantized_parameter_size = None
 
     def train(self, device):
@@ -70,9 +72,7 @@ class FedQuantWorker(Worker):
         trainer = kwargs["model_executor"]
         payload = self.quantized_parameters()
         if self.quantized_parameter_size is None:
-            self.quantized_parameter_size = sum(
-                (v[0].numel() + 8 * v[1].numel()) if isinstance(v, tuple) else 4 * v.numel()
-                for v in payload.values())
+            self.quantized_parameter_size = get_data_serialization_size(payload)
         log.warning("parameter_size is %s, quantized_parameter_size is %s, compression ratio is %s",
                     self.parameter_size, self.quantized_parameter_size,
                     float(self.quantized_parameter_size) / float(self.parameter_size))

@@ -1,7 +1,9 @@
-"""GPU: the sharded servers with the real HIP kernels, 2 ranks on one GPU over gloo.
+"""GPU: the sharded servers with the real HIP kernels, 2 ranks, two rounds each.
 
-(RCCL needs one GPU per rank, so the single-GPU test box exercises the same
-code path with the gloo backend; the collectives are the same calls.)
+``gloo``: both ranks on one GPU (the single-GPU test box).  ``nccl`` (RCCL over
+xGMI): one GPU per rank, run where two GPUs are visible and skipped otherwise;
+the collectives are the same calls.  Every round's broadcast must be retired by
+the rank's local workers (no round result left in the queue).
 """
 import os
 import socket
@@ -25,10 +27,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outq):
+def _worker(rank, world, port, backend, outq):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(rank if backend == "nccl" else 0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     from distributed_learning_simulator_amd.distributed import (ShardedFedQuantServer,
                                                                 ShardedFedServer,
                                                                 ShardedSignSGDServer)
@@ -39,13 +41,20 @@ def _worker(rank, world, port, outq):
     k, layout, K = case["key"], case["layout"], case["K"]
     U, n = z[f"{k}_U"], z[f"{k}_n"]
     s = ShardedFedServer(tester=None, worker_number=K, synchronous=True)
-    for wid in s.local_worker_ids:
-        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
-        s.worker_data_queue.add_task((wid, int(n[wid]), d))
-    for w in s.local_worker_ids:
-        s.worker_data_queue.get_result(consumer=w, timeout=60)
-    res = s.worker_data_queue.get_result(consumer=s.local_worker_ids[0], timeout=60)
-    out["fed"] = np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout])
+    q = s.worker_data_queue
+    for w in s.local_worker_ids:  # the initial broadcast
+        q.get_result(consumer=w, timeout=60)
+    fed = []
+    for _round in range(2):
+        for wid in s.local_worker_ids:
+            d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
+            q.add_task((wid, int(n[wid]), d))
+        for w in s.local_worker_ids:
+            res = q.get_result(consumer=w, timeout=60)
+        assert len(q._results) == 0, "round result left in the queue"
+        fed.append(np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout]))
+    assert np.array_equal(fed[0].view(np.uint32), fed[1].view(np.uint32))
+    out["fed"] = fed[0]
     # sign vote
     zs = G.load("sign_vote.npz")
     cs = G.meta(zs)[1]
@@ -60,26 +69,36 @@ def _worker(rank, world, port, outq):
     zq = G.load("dequant.npz")
     cq = G.meta(zq)[0]
     sq = ShardedFedQuantServer(tester=None, worker_number=cq["K"], synchronous=True)
-    for i in sq.local_worker_ids:
-        d = {}
-        for name, shape in cq["layout"]:
-            if name in cq["qnames"]:
-                d[name] = tuple(torch.from_numpy(zq[f"q{i}_{name}_{x}"].copy())
-                                for x in ("int", "scale", "zp"))
-            else:
-                d[name] = torch.from_numpy(zq[f"q{i}_{name}_f32"].copy())
-        sq.worker_data_queue.add_task((i, int(zq["n"][i]), d))
+    qq = sq.worker_data_queue
+    for w in sq.local_worker_ids:  # the initial broadcast
+        qq.get_result(consumer=w, timeout=60)
+    for _round in range(2):
+        for i in sq.local_worker_ids:
+            d = {}
+            for name, shape in cq["layout"]:
+                if name in cq["qnames"]:
+                    d[name] = tuple(torch.from_numpy(zq[f"q{i}_{name}_{x}"].copy())
+                                    for x in ("int", "scale", "zp"))
+                else:
+                    d[name] = torch.from_numpy(zq[f"q{i}_{name}_f32"].copy())
+            qq.add_task((i, int(zq["n"][i]), d))
+        for w in sq.local_worker_ids:
+            qq.get_result(consumer=w, timeout=60)
+        assert len(qq._results) == 0, "fed_quant round result left in the queue"
     agg = sq.last_aggregate
     out["quant"] = np.concatenate([agg[nm].reshape(-1).cpu().numpy() for nm, _ in cq["layout"]])
     outq.put((rank, out))
     dist.destroy_process_group()
 
 
-def test_sharded_servers_two_ranks_one_gpu():
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_sharded_servers_two_ranks(backend):
+    if backend == "nccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one GPU per rank")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, backend, q)) for r in range(2)]
     for p in procs:
         p.start()
     outs = dict(q.get(timeout=170) for _ in range(2))

@@ -318,3 +318,20 @@ def test_shapley_host_logic_config5_scale(doubles, tag, tmp_path):
     assert {tuple(s) for s in server.evaluated_subsets} == set(case["evaluated"])
     if not gtg:
         assert (tmp_path / "metric_1").read_bytes() == case["metric_pickle"]
+
+
+def test_data_serialization_size_matches_pickle():
+    """The compression-ratio sizes (ref servers/fed_quant_server.py:41-42,
+    workers/fed_quant_worker.py:28-30,43) are len(pickle.dumps(payload)) of the
+    CPU payload, whatever its values."""
+    import pickle
+
+    from distributed_learning_simulator_amd.model_util import get_data_serialization_size
+    g = torch.Generator().manual_seed(3)
+    params = {"conv.weight": torch.randn(16, 3, 3, 3, generator=g), "fc.bias": torch.randn(10, generator=g)}
+    q = {"conv.weight": (torch.randint(-128, 128, (16, 3, 3, 3), dtype=torch.int8, generator=g),
+                         torch.rand(16, generator=g), torch.zeros(16, dtype=torch.int32)),
+         "fc.bias": torch.randn(10, generator=g)}
+    for data in (params, q, (torch.zeros(100, dtype=torch.uint8), torch.ones(3), torch.zeros(3, dtype=torch.int32))):
+        assert get_data_serialization_size(data) == len(pickle.dumps(data))
+    assert get_data_serialization_size(q) < get_data_serialization_size(params)

@@ -19,9 +19,16 @@ def build(name, defs, src=CSRC):
     d = os.path.join(OUT, name)
     os.makedirs(d, exist_ok=True)
     objs = []
+    # DLS_VARIANT_SRCS=a.hip,b.hip: compile only those, link the in-tree build's
+    # objects of the others (the knob does not touch them)
+    only = [x for x in os.environ.get("DLS_VARIANT_SRCS", "").split(",") if x]
     for s in SRCS:
         o = os.path.join(d, s.replace(".hip", ".o"))
-        subprocess.check_call(["hipcc", *FLAGS, *defs, "-I", src, "-c", os.path.join(src, s), "-o", o])
+        if only and s not in only:
+            o = os.path.join(CSRC, "_build", s.replace(".hip", ".o"))
+        else:
+            subprocess.check_call(["hipcc", *FLAGS, *defs, "-I", src, "-c", os.path.join(src, s),
+                                   "-o", o])
         objs.append(o)
     lib = os.path.join(OUT, f"libdls_{name}.so")
     subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, *objs])
