@@ -413,9 +413,13 @@ def bench_shapley_exact(args, dev):
     wall, kms = timed_launches(step, args.steps, args.warmup)
     ms = wall / args.steps * 1e3
     pairs = sum(len(c) for c in subs)
-    # minimum VALU lane-ops: per parameter, 4 per (client, coalition) membership
-    # (Markstein q0, r, q + the add) and 1 per client for t = x * n_i
-    valu_ops = layout.numel * (4 * pairs + K)
+    # minimum VALU lane-ops: per parameter, per (client, coalition) membership the
+    # quotient (two-constant 2 ops where proven for the coalition's N, else
+    # Markstein's 3) + the add, and 1 per client for t = x * n_i
+    from distributed_learning_simulator_amd._native import two_constant_division
+    per_member = sum(len(c) * (1 + (2 if two_constant_division(float(sum(n[k] for k in c))) else 3))
+                     for c in subs)
+    valu_ops = layout.numel * (per_member + K)
     bytes_per_launch = (K + S) * P * 4
     # the per-coalition kernel on the same batch, for comparison
     off, fr, fw, ft = [0], [], [], []
@@ -526,12 +530,39 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
         el = _max_over_ranks(el, dev)
     n = len(coal) - 2 * world
     del server
+    torch.cuda.empty_cache()
+    bn = bench_bn_act(args, dev) if rank == 0 else None
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
                       f"{args.eval_images} CIFAR-10-shaped images (fp32, NHWC, batch 1000)",
             "value": round(n / el, 3), "unit": "subset-evals/s (all GPUs)",
             "ms_per_eval_per_gpu": round(el / n * world * 1e3, 2),
-            "utility_range": [round(min(vals), 4), round(max(vals), 4)]}
+            "utility_range": [round(min(vals), 4), round(max(vals), 4)],
+            "bn_act": bn}
+
+
+def bench_bn_act(args, dev):
+    """The utility inference's hand-written pass (dls_bn_act_nhwc_f32): eval batch
+    norm + residual add + ReLU over ResNet-18's largest activation, a batch of
+    1000 CIFAR images x 64 channels x 32 x 32 (channels_last); 12 B per element."""
+    x = torch.randn(1000, 64, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x)
+    y = torch.empty_like(x)
+    a = torch.rand(64, device=dev) + 0.5
+    b = torch.randn(64, device=dev)
+
+    def step(ea=None, eb=None):
+        if ea is not None:
+            ea.record()
+        _native.bn_act_nhwc(x, a, b, residual=r, relu=True, out=y)
+        if eb is not None:
+            eb.record()
+
+    _, kms = timed_launches(step, max(10, args.steps), 3)
+    nbytes = x.numel() * 12
+    del x, r, y
+    return {"config": "eval BN + residual + ReLU, [1000, 64, 32, 32] fp32 channels_last",
+            "roofline": roofline("dls_bn_act_nhwc_f32", nbytes, kms, key="bn_act")}
 
 
 # ---------------------------------------------------------- CPU baseline

@@ -69,6 +69,8 @@ SIGNATURES = {
     "dls_qparams_minmax": ([_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p], _i32),
     "dls_quantize_affine": ([_p, _p, _i32, _p, _p, _i32, _i32, _p, _p, _i32, _u64, _i64, _p],
                             _i32),
+    "dls_bn_fold_f32": ([_p, _p, _p, _p, _f32, _i32, _p, _p, _p], _i32),
+    "dls_bn_act_nhwc_f32": ([_p, _i64, _i32, _p, _p, _p, _i32, _p, _p], _i32),
 }
 
 _lib = None
@@ -256,3 +258,29 @@ def quantize(x, seg_off, total, scale, zp, q, deq=None, qmin=0, qmax=255, stocha
 def quantize_u8(x, seg_off, total, scale, zp, q, deq=None, stochastic=False, seed=0,
                 stream=None):
     quantize(x, seg_off, total, scale, zp, q, deq, 0, 255, stochastic, seed, stream)
+
+
+# ----------------------------------------------------------- utility evaluation
+def bn_fold(bn, alpha, beta, stream=None):
+    """Eval-mode constants of a BatchNorm module (dls_bn_fold_f32) into alpha, beta [C]."""
+    _check(lib().dls_bn_fold_f32(_ptr(bn.weight), _ptr(bn.bias), _ptr(bn.running_mean),
+                                 _ptr(bn.running_var), float(bn.eps), bn.num_features,
+                                 _ptr(alpha), _ptr(beta), _stream(stream, alpha)),
+           "dls_bn_fold_f32")
+
+
+def bn_act_nhwc(x, alpha, beta, residual=None, relu=True, out=None, inplace=False, stream=None):
+    """y = act(x * alpha + beta [+ residual]) over a channels_last [N, C, H, W] fp32
+    activation in one pass (dls_bn_act_nhwc_f32); returns y (channels_last;
+    x itself when inplace)."""
+    N, C, H, W = x.shape
+    cl = torch.channels_last
+    if not x.is_contiguous(memory_format=cl) or (
+            residual is not None and not residual.is_contiguous(memory_format=cl)):
+        raise RuntimeError("bn_act_nhwc: activations must be channels_last contiguous")
+    if out is None:
+        out = x if inplace else torch.empty_like(x, memory_format=cl)
+    _check(lib().dls_bn_act_nhwc_f32(_ptr(x), N * H * W, C, _ptr(alpha), _ptr(beta),
+                                     _ptr(residual), int(bool(relu)), _ptr(out),
+                                     _stream(stream, x)), "dls_bn_act_nhwc_f32")
+    return out

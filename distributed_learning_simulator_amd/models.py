@@ -42,6 +42,20 @@ class _Block(nn.Module):
         out = self.bn2(self.conv2(out))
         return F.relu(out + self.shortcut(x))
 
+    def forward_fused(self, x, fold):
+        """Eval-mode forward on channels_last activations: each batch norm (with the
+        ReLU / residual add after it) is one dls_bn_act_nhwc_f32 pass, in place on
+        the convolution's output; same op order as forward()."""
+        from . import _native
+        out = _native.bn_act_nhwc(self.conv1(x), *fold[id(self.bn1)], relu=True, inplace=True)
+        out = self.conv2(out)
+        if len(self.shortcut):
+            sc = _native.bn_act_nhwc(self.shortcut[0](x), *fold[id(self.shortcut[1])], relu=False,
+                                     inplace=True)
+        else:
+            sc = x
+        return _native.bn_act_nhwc(out, *fold[id(self.bn2)], residual=sc, relu=True, inplace=True)
+
 
 class ResNet18(nn.Module):
     """CIFAR-10 ResNet-18 (3x3 stem, no max-pool)."""
@@ -64,6 +78,32 @@ class ResNet18(nn.Module):
     def forward(self, x):
         out = F.relu(self.bn1(self.conv1(x)))
         out = self.layer4(self.layer3(self.layer2(self.layer1(out))))
+        out = F.adaptive_avg_pool2d(out, 1).flatten(1)
+        return self.linear(out)
+
+    @torch.no_grad()
+    def fold_bn(self):
+        """{id(bn): (alpha, beta)} of every batch norm for forward_fused (eval mode,
+        running statistics; recomputed per evaluation since the weights change)."""
+        from . import _native
+        fold = {}
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                a = torch.empty(m.num_features, device=m.running_mean.device)
+                b = torch.empty_like(a)
+                _native.bn_fold(m, a, b)
+                fold[id(m)] = (a, b)
+        return fold
+
+    def forward_fused(self, x, fold):
+        """forward() for utility evaluation on the GPU: channels_last activations,
+        MIOpen convolutions, every batch norm + ReLU (+ residual add) fused into one
+        hand-written pass (dls_bn_act_nhwc_f32)."""
+        from . import _native
+        out = _native.bn_act_nhwc(self.conv1(x), *fold[id(self.bn1)], relu=True, inplace=True)
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                out = blk.forward_fused(out, fold)
         out = F.adaptive_avg_pool2d(out, 1).flatten(1)
         return self.linear(out)
 

@@ -63,6 +63,11 @@ class Inferencer:
             # NHWC convolutions: measured 8-18 % faster than NCHW for this model family
             # on MI355X (tools/eval_probe.py); results are the same up to fp32 reassociation
             self.model.to(memory_format=torch.channels_last)
+        # models with a fused eval forward (models.ResNet18): every batch norm + ReLU
+        # (+ residual add) is one hand-written NHWC pass instead of three kernels
+        fused = (getattr(self.model, "forward_fused", None)
+                 if X.dim() == 4 and torch.device(self.device).type == "cuda" else None)
+        fold = self.model.fold_bn() if fused is not None else None
         correct = torch.zeros((), dtype=torch.int64, device=self.device)
         loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         for i in range(0, X.shape[0], self.batch_size):
@@ -70,7 +75,7 @@ class Inferencer:
             yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
             if xb.dim() == 4 and xb.is_cuda:
                 xb = xb.contiguous(memory_format=torch.channels_last)
-            out = self.model(xb)
+            out = fused(xb, fold) if fused is not None else self.model(xb)
             loss_sum += torch.nn.functional.cross_entropy(out, yb, reduction="sum").double()
             correct += (out.argmax(1) == yb).sum()
         n = X.shape[0]

@@ -223,6 +223,22 @@ int dls_quantize_affine(const float *x, const int64_t *seg_off, int32_t nseg, co
                         const int32_t *zp, int32_t qmin, int32_t qmax, void *q, float *deq,
                         int32_t stochastic, uint64_t seed, int64_t total, dls_stream_t stream);
 
+/* ------------------------------------------------------- utility evaluation
+ * Eval-mode batch norm for the Shapley servers' utility inference
+ * (servers/fed_server.py:26-32 get_metric -> tester.inference()).
+ * dls_bn_fold_f32: per channel alpha = fl(invstd * w), beta = fl(b - fl(mean * alpha)),
+ * invstd = fl(1 / fl(sqrt(fl(var + eps)))) (ATen's CPU inference constants);
+ * weight / bias may be null (affine=False: w = 1, b = 0).
+ * dls_bn_act_nhwc_f32: y = fl(fl(x * alpha_c) + beta_c), then + residual (if
+ * not null) and ReLU (if relu) over a channels_last [rows = N*H*W, C] fp32
+ * tensor in one pass; C a multiple of 4, 16-byte aligned pointers; y may
+ * alias x. */
+int dls_bn_fold_f32(const float *weight, const float *bias, const float *mean, const float *var,
+                    float eps, int32_t C, float *alpha, float *beta, dls_stream_t stream);
+int dls_bn_act_nhwc_f32(const float *x, int64_t rows, int32_t C, const float *alpha,
+                        const float *beta, const float *residual, int32_t relu, float *y,
+                        dls_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,103 @@
+"""GPU: the utility-evaluation inference path (get_metric,
+servers/fed_server.py:26-32) with its hand-written eval batch norm.
+
+* dls_bn_fold_f32 / dls_bn_act_nhwc_f32 against the same fp32 op sequence in
+  torch (alpha = 1/sqrt(var+eps) * w, beta = b - mean * alpha, y = x*alpha + beta,
+  + residual, ReLU): bit-exact, every flag combination, ragged sizes, C not a
+  divisor of the grid (the per-iteration channel path), in place.
+* ResNet-18 forward_fused vs torch's own eval forward (MIOpen batch norm):
+  logits within 1e-4 (relative, normwise per image) and identical predictions
+  on all but near-tied images; the Inferencer's accuracy equal.  Utility parity
+  with the reference's tester is unpinned (its library is absent).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+
+
+def _bn(C, g):
+    bn = torch.nn.BatchNorm2d(C).to(dev).eval()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(C, generator=g) * 0.2)
+        bn.running_var.copy_(torch.rand(C, generator=g) + 0.1)
+    return bn
+
+
+def _ref_fold(bn):
+    invstd = 1.0 / torch.sqrt(bn.running_var + bn.eps)
+    a = invstd * bn.weight
+    return a, bn.bias - bn.running_mean * a
+
+
+@pytest.mark.parametrize("N,C,H,W", [(3, 64, 7, 5), (2, 96, 3, 3), (5, 512, 4, 4), (1, 12, 1, 1)])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False), (True, False)])
+def test_bn_act_bit_exact(N, C, H, W, res, relu):
+    from distributed_learning_simulator_amd import _native
+    g = torch.Generator().manual_seed(N * C + H)
+    bn = _bn(C, g)
+    a = torch.empty(C, device=dev)
+    b = torch.empty(C, device=dev)
+    _native.bn_fold(bn, a, b)
+    ra, rb = _ref_fold(bn)
+    assert torch.equal(a.view(torch.int32), ra.detach().view(torch.int32))
+    assert torch.equal(b.view(torch.int32), rb.detach().view(torch.int32))
+    cl = torch.channels_last
+    x = torch.randn(N, C, H, W, generator=g).to(dev).contiguous(memory_format=cl)
+    x[0, 0, 0, 0] = float("nan")
+    r = torch.randn(N, C, H, W, generator=g).to(dev).contiguous(memory_format=cl) if res else None
+    y = _native.bn_act_nhwc(x, a, b, residual=r, relu=relu)
+    ref = x * a[None, :, None, None] + b[None, :, None, None]
+    if res:
+        ref = ref + r
+    if relu:
+        ref = torch.relu(ref)
+    assert y.is_contiguous(memory_format=cl)
+    assert torch.isnan(y[0, 0, 0, 0])
+    m = ~torch.isnan(ref)
+    assert torch.equal(y[m].view(torch.int32), ref[m].view(torch.int32))
+    y2 = _native.bn_act_nhwc(x.clone(memory_format=cl), a, b, residual=r, relu=relu, inplace=True)
+    assert torch.equal(y2[m].view(torch.int32), ref[m].view(torch.int32))
+
+
+def test_bn_act_rejects_nchw():
+    from distributed_learning_simulator_amd import _native
+    x = torch.randn(2, 8, 3, 3, device=dev)
+    with pytest.raises(RuntimeError):
+        _native.bn_act_nhwc(x, torch.ones(8, device=dev), torch.zeros(8, device=dev))
+
+
+def test_resnet18_fused_eval_matches_torch():
+    from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    torch.manual_seed(0)
+    model = ResNet18().to(dev)
+    g = torch.Generator().manual_seed(1)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.weight.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    X, y = synthetic_classification(600, (3, 32, 32), seed=3)
+    model.eval().to(memory_format=torch.channels_last)
+    xb = X.to(dev).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        ref = model(xb)
+        got = model.forward_fused(xb, model.fold_bn())
+    err = torch.linalg.norm(got - ref, dim=1) / torch.linalg.norm(ref, dim=1)
+    assert float(err.max()) < 1e-4, float(err.max())
+    top2 = torch.topk(ref, 2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 1e-3 * top2[:, 0].abs().clamp_min(1e-6)
+    assert torch.equal(got.argmax(1)[clear], ref.argmax(1)[clear])
+    # the Inferencer takes the fused path on the GPU; accuracy as torch's forward
+    inf = Inferencer(model, (X, y), batch_size=256, device=dev)
+    _, acc, _ = inf.inference()
+    ref_acc = float((ref.argmax(1).cpu() == y).float().mean())
+    assert abs(acc - ref_acc) <= 2 / 600
+    assert np.isfinite(float(inf.loss_metric.value))

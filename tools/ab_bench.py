@@ -33,7 +33,9 @@ def load(path):
     # libraries named libdls_oldabi*.so predate nfast[4] (they take the fast-tile total)
     L.old_nfast = os.path.basename(path).startswith("libdls_oldabi")
     for name, (args, res) in _native.SIGNATURES.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)  # a variant built from an older tree may lack newer entry points
+        if f is None:
+            continue
         f.argtypes = args
         f.restype = res
     if L.old_nfast:
@@ -212,6 +214,15 @@ def setup(dev, want=()):
                                                            ptr(t_fw), ptr(t_ft), 50, P, ptr(uo), P,
                                                            stream()), 100 * P * 4)
     print("union member pairs", pairs, flush=True)
+    if "bn_act" in want:  # utility inference: eval BN + residual + ReLU, largest ResNet-18 activation
+        bx = torch.randn(1000, 64, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
+        br = torch.randn_like(bx)
+        by = torch.empty_like(bx)
+        ba = torch.rand(64, device=dev) + 0.5
+        bb = torch.randn(64, device=dev)
+        W["bn_act"] = (lambda L: L.dls_bn_act_nhwc_f32(ptr(bx), 1000 * 32 * 32, 64, ptr(ba), ptr(bb),
+                                                        ptr(br), 1, ptr(by), stream()),
+                       bx.numel() * 12)
     C = torch.rand((50, 50), generator=g, device=dev)
     C = C / C.sum(1, keepdim=True)
     go = torch.empty((50, P), device=dev)

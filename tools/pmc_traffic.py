@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CALLS = 3
 KEYS = {"fedavg": "headline", "fedavg1k": "fedavg_k1000", "vote_sign": "sign_vote",
         "pack": "sign_pack", "quant": "fed_quant", "quant_r18": "fed_quant_k1000",
-        "union": "shapley_exact", "gemm": "shapley_gemm"}
+        "union": "shapley_exact", "gemm": "shapley_gemm", "bn_act": "bn_act"}
 
 
 def sums(path):
