@@ -223,21 +223,8 @@ __global__ __launch_bounds__(kBlock) void k_subset_exact(const f32x4 *__restrict
 //   acc_s = fl(acc_s + fl(t_j / N_s)) for the members j of coalition s, in union order
 // which is term for term the op sequence of servers/fed_server.py:57-65 for
 // each coalition (acc_s starts at -0: -0 + q == q, "the first client is assigned").
-//
-// Persistent blocks of kUnionWaves waves walk 256-parameter tiles (a lane owns 4
-// parameters).  Per tile the waves stage t_j of the <= 64 clients in LDS (each
-// wave a few clients, register-staged: the NEXT tile's rows are loaded while
-// this tile is computed, so HBM latency hides behind a whole tile of work);
-// then wave w computes its coalitions (w, w + W, ...) coalition-major: it walks
-// the coalition's member list (built once per block in LDS from the member
-// masks) with 4 independent Markstein quotients in flight and the adds in list
-// order.  No per-membership branches; a wave's results are stored at the start
-// of the next tile, just before that tile's loads are issued, so the loads never
-// wait behind younger stores (vmcnt counts both, in order).
-// Algorithmic bytes: (Ku + S) * 4 per parameter.  VALU per parameter: 4 per
-// (client, coalition) membership (Markstein's 3 + the add) + 1 per client for t;
-// at S = Ku = 50 with half-full coalitions the VALU issue, not HBM, is the roof
-// (DESIGN.md §4).
+// Algorithmic bytes: (Ku + S) * 4 per parameter; VALU: per parameter and
+// membership the quotient (2 ops two-constant / 3 Markstein) + the add.
 constexpr int kUnionChunk = 64;  // clients per launch (the host splits larger unions)
 
 // in_fast_range (dls_common.h) of all four: 2^-60 <= |t| < 2^61 on the bit
@@ -248,12 +235,7 @@ __device__ __forceinline__ bool all_in_fast_range(f32x4 t) {
     const uint32_t mn = min(min(a, b), min(c, d)), mx = max(max(a, b), max(c, d));
     return mn >= (67u << 23) && mx < (188u << 23);
 }
-constexpr int kUnionWaves = 8;   // waves per block: <= 8 clients staged, <= KW coalitions each
 
-// KW = ceil(S / 8) coalitions per wave (a template parameter, so that every wave
-// issues exactly KW stores and NL loads per tile: the compiler's vmcnt waits
-// are then exact, and waiting for the next tile's loads never waits for this
-// tile's younger stores).
 // Per-coalition division constants, computed on the host (dls_common.h FastDiv):
 // {yh = RN(1/N), yl = RN(1/N - yh), N, flags}; flags bit 0: the two-constant
 // quotient fma(t, yh, RN(t * yl)) is proven correctly rounded for this N (the
@@ -262,313 +244,8 @@ struct UnionDiv {
     f32x4 c[DLS_SUBSET_UNION_MAX];
 };
 
-template <int KW, bool ACC>
-__global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
-    const f32x4 *__restrict__ Uv, int64_t ldu4, const int32_t *__restrict__ urows,
-    const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku, UnionDiv dv, int S,
-    int64_t P4, int64_t ntiles, f32x4 *__restrict__ out, int64_t ldo4) {
-    constexpr int W = kUnionWaves, NL = kUnionChunk / kUnionWaves;
-    // 69 KiB in all, so two blocks (16 waves) share a CU
-    __shared__ f32x4 ts[kUnionChunk * 64];                    // 64 KiB: t_j of this tile
-    __shared__ uint8_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk];  // member positions, per coalition
-    __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];               // UnionDiv, per coalition
-    __shared__ uint32_t tbad[W];                              // per loader wave: t out of range
-    int64_t tile = blockIdx.x;
-    if (tile >= ntiles) return;  // block-uniform
-    const int lane = __lane_id();
-    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // client table: lane j holds client j's row and weight
-    const int kk = min(lane, Ku - 1);
-    const int tr = urows[kk];
-    const float tw = uw[kk];
-    const uint64_t mj = lane < Ku ? member[kk] : 0ull;
-    // this wave's coalitions: wv + W k (k < nk); a wave without one (S < 8)
-    // recomputes coalition S - 1 (the same bits, stored twice)
-    int nk = (S - wv + W - 1) / W;
-    const int cdup = nk > 0 ? -1 : S - 1;
-    nk = nk > 0 ? nk : 1;
-    auto coal = [&](int k) { return cdup >= 0 ? cdup : wv + W * k; };
-    int len[KW];
-    int fast = (int)(__ballot(!(tw >= 1.0f && tw <= 16777216.0f)) == 0);  // 1 <= n_j <= 2^24
-#pragma unroll
-    for (int k = 0; k < KW; ++k) {
-        len[k] = 0;
-        if (k < nk) {
-            const int c = coal(k);
-            const uint64_t in = __ballot((mj >> c) & 1ull);
-            len[k] = __popcll(in);
-            if (cdup < 0) {  // one wave builds each coalition's tables
-                if ((mj >> c) & 1ull)
-                    lst[c][__builtin_amdgcn_mbcnt_hi((uint32_t)(in >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)in, 0u))] =
-                        (uint8_t)lane;
-                if (lane == 0) cst[c] = dv.c[c];
-            }
-            fast &= (int)((__float_as_uint(dv.c[c].w) & 2u) != 0);
-        }
-    }
-    // loader slots: wave wv stages clients wv + W l, l < NL (past Ku: a duplicate
-    // row, loaded but never staged, so the load count is static)
-    f32x4 R[NL];
-    auto issue = [&](int64_t t) {
-        const int64_t i0 = t * 64 + lane;
-        const int64_t iq = i0 < P4 ? i0 : P4 - 1;
-#pragma unroll
-        for (int l = 0; l < NL; ++l) {
-            const int j = min(wv + W * l, Ku - 1);
-            const int64_t r = __builtin_amdgcn_readlane(tr, j);
-            R[l] = load4<false>(Uv + r * ldu4 + iq);
-        }
-    };
-    f32x4 ain[KW];  // ACC: running sums of a previous 64-client chunk
-    auto load_acc = [&](int64_t t) {
-        const int64_t i0 = t * 64 + lane;
-        const int64_t iq = i0 < P4 ? i0 : P4 - 1;
-#pragma unroll
-        for (int k = 0; k < KW; ++k)
-            ain[k] = out[(int64_t)coal(k < nk ? k : nk - 1) * ldo4 + iq];
-    };
-    if (ACC) load_acc(tile);
-    issue(tile);
-    for (; tile < ntiles; tile += gridDim.x) {
-        const int64_t i0 = tile * 64 + lane;
-        const int64_t iq = i0 < P4 ? i0 : P4 - 1;
-        __syncthreads();  // every wave is done reading the previous tile's t (and the tables)
-        uint32_t bad = 0;
-#pragma unroll
-        for (int l = 0; l < NL; ++l) {
-            const int j = wv + W * l;
-            if (j < Ku) {
-                const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
-                f32x4 t;
-                t.x = R[l].x * wk;
-                t.y = R[l].y * wk;
-                t.z = R[l].z * wk;
-                t.w = R[l].w * wk;
-                ts[j * 64 + lane] = t;
-                bad |= (uint32_t)(__ballot(!all_in_fast_range(t)) != 0);
-            }
-        }
-        if (lane == 0) tbad[wv] = bad;
-        f32x4 acc_in[KW];
-#pragma unroll
-        for (int k = 0; k < KW; ++k)
-            acc_in[k] = ACC ? ain[k] : f32x4{-0.f, -0.f, -0.f, -0.f};
-        // the next tile's rows (the last tile reloads itself: a static load count)
-        const int64_t next = tile + gridDim.x < ntiles ? tile + gridDim.x : tile;
-        if (ACC) load_acc(next);
-        issue(next);  // in flight during this tile's compute
-        __syncthreads();
-        uint32_t anybad = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) anybad |= tbad[w];
-        // Common case: every t of the tile in Markstein's range and every divisor in
-        // [1, 2^31].  Otherwise (zeros, denormals, huge values, inf / nan) a compact
-        // slow path with guarded division.  Both issue exactly KW stores.
-        const bool tile_fast = fast && anybad == 0;
-        f32x4 last = acc_in[0];
-        int64_t lrow = (int64_t)coal(0) * ldo4;
-#pragma unroll
-        for (int k = 0; k < KW; ++k) {
-            if (k < nk) {  // wave-uniform
-                const int c = coal(k);
-                f32x4 acc = acc_in[k];
-                if (__builtin_expect(tile_fast, 1)) {
-                    const f32x4 cc = cst[c];
-                    const f32x2 y2 = f32x2{cc.x, cc.x}, l2 = f32x2{cc.y, cc.y};
-                    const f32x2 b2 = f32x2{cc.z, cc.z};
-                    const bool two = (__float_as_uint(cc.w) & 1u) != 0;  // wave-uniform
-                    const uint32_t vl = (uint32_t)lst[c][lane] << 10;  // lane l: member l's offset
-                    const int n = len[k];
-                    // q = RN(t / N): two-constant (2 ops) when proven for N, else
-                    // Markstein (3 ops); element pairs in v_pk_* (the scalar roundings)
-                    auto quot = [&](f32x4 t) {
-                        const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
-                        f32x2 ql, qh;
-                        if (two) {
-                            ql = __builtin_elementwise_fma(tl, y2, tl * l2);
-                            qh = __builtin_elementwise_fma(th, y2, th * l2);
-                        } else {
-                            const f32x2 ql0 = tl * y2, qh0 = th * y2;
-                            ql = __builtin_elementwise_fma(__builtin_elementwise_fma(-ql0, b2, tl),
-                                                           y2, ql0);
-                            qh = __builtin_elementwise_fma(__builtin_elementwise_fma(-qh0, b2, th),
-                                                           y2, qh0);
-                        }
-                        return f32x4{ql.x, ql.y, qh.x, qh.y};
-                    };
-                    auto tload = [&](int l) {
-                        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)vl, l);
-                        return *reinterpret_cast<const f32x4 *>(
-                            reinterpret_cast<const char *>(ts) + off + 16 * lane);
-                    };
-                    int l = 0;
-                    if (n >= 4) {
-                        // groups of 4 members: the next group's t are read from LDS
-                        // while this group's 4 independent quotients are computed;
-                        // the adds stay in member order
-                        f32x4 x0 = tload(0), x1 = tload(1), x2 = tload(2), x3 = tload(3);
-                        for (; l + 8 <= n; l += 4) {
-                            const f32x4 z0 = tload(l + 4), z1 = tload(l + 5);
-                            const f32x4 z2 = tload(l + 6), z3 = tload(l + 7);
-                            const f32x4 q0 = quot(x0), q1 = quot(x1), q2 = quot(x2), q3 = quot(x3);
-                            acc = add4(add4(add4(add4(acc, q0), q1), q2), q3);
-                            x0 = z0;
-                            x1 = z1;
-                            x2 = z2;
-                            x3 = z3;
-                        }
-                        const f32x4 q0 = quot(x0), q1 = quot(x1), q2 = quot(x2), q3 = quot(x3);
-                        acc = add4(add4(add4(add4(acc, q0), q1), q2), q3);
-                        l += 4;
-                    }
-                    for (; l < n; ++l) acc = add4(acc, quot(tload(l)));
-                } else {
-                    const f32x4 cc = cst[c];
-                    FastDiv d;
-                    d.b = cc.z;
-                    d.y = cc.x;
-                    d.fast = (__float_as_uint(cc.w) & 2u) != 0;
-                    for (int j = 0; j < Ku; ++j) {
-                        if (!__builtin_amdgcn_readlane((int)((mj >> c) & 1ull), j)) continue;
-                        const f32x4 t = ts[j * 64 + lane];
-                        for (int e = 0; e < 4; ++e)
-                            acc[e] += (d.fast && in_fast_range(t[e])) ? markstein(t[e], d.b, d.y)
-                                                                      : t[e] / d.b;
-                    }
-                }
-                last = acc;
-                lrow = (int64_t)c * ldo4;
-            }
-            // exactly KW stores per wave and tile (past nk: the last one again; lanes
-            // past P hold column P-1's value, iq: the same bits stored twice)
-            out[lrow + iq] = last;
-        }
-    }
-}
-
-// Register-resident form: one wave per tile of 64*V parameters (a lane owns V
-// consecutive ones), no LDS and no barriers.  The wave loads the tile's slice of
-// all Ku client rows into registers (t[j], V*KU VGPRs), forms t_j = fl(x_j * n_j)
-// in place, then walks the S coalitions one after another: coalition s's member
-// mask over the union (a wave-uniform 64-bit ballot of the per-client coalition
-// masks) drives a statically unrolled j loop whose scalar branches skip the
-// non-members, so t[j] stays a static register and the adds follow union order.
-// Per membership and element: the quotient (2 ops two-constant / 3 Markstein)
-// and the add, nothing else; per (coalition, client) pair one scalar test.
-// A tile with any t outside Markstein's range, or a coalition whose divisor is
-// outside [1, 2^31], takes IEEE division for that coalition.
-#ifndef DLS_UNION_REG
-#define DLS_UNION_REG 2
-#endif
-#ifndef DLS_UNION_V
-#define DLS_UNION_V 2
-#endif
-#ifndef DLS_UNION_SEL
-#define DLS_UNION_KEEP_BRANCH asm volatile("")
-#else
-#define DLS_UNION_KEEP_BRANCH
-#endif
-constexpr int kUnionRegBlock = 256;
-
-template <int V, int KU, bool ACC>
-__global__ __launch_bounds__(kUnionRegBlock) void k_subset_union_reg(
-    const float *__restrict__ U, int64_t ldu, const int32_t *__restrict__ urows,
-    const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku, UnionDiv dv, int S,
-    int64_t PV, float *__restrict__ out, int64_t ldo) {
-    typedef float vf __attribute__((ext_vector_type(V)));
-    const vf *__restrict__ Uv = reinterpret_cast<const vf *>(U);
-    vf *__restrict__ ov = reinterpret_cast<vf *>(out);
-    const int64_t ldv = ldu / V, ldov = ldo / V;
-    const int lane = __lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * (kUnionRegBlock / 64) + (threadIdx.x >> 6);
-    if (tile * 64 >= PV) return;  // wave-uniform
-    const int64_t i0 = tile * 64 + lane;
-    const int64_t iq = i0 < PV ? i0 : PV - 1;
-    const int kk = min(lane, Ku - 1);
-    const int tr = urows[kk];
-    const float tw = uw[kk];
-    const uint64_t mj = lane < Ku ? member[kk] : 0ull;
-    // wave-uniform row base in a buffer descriptor (SALU) + the lane's 32-bit
-    // byte offset: no 64-bit address VGPRs per client
-    const int boff = (int)((uint32_t)iq * (uint32_t)sizeof(vf));
-    vf t[KU];
-#pragma unroll
-    for (int j = 0; j < KU; ++j) {
-        // past Ku: client Ku-1's slice again (same lines, a static load count)
-        const int64_t r = __builtin_amdgcn_readlane(tr, j < Ku ? j : Ku - 1);
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<vf *>(Uv + r * ldv), 0,
-                                                          (int)0xffffffffu, 0x00020000);
-        if constexpr (V == 2)
-            t[j] = __builtin_bit_cast(vf, __builtin_amdgcn_raw_buffer_load_b64(rs, boff, 0, 0));
-        else
-            t[j] = __builtin_bit_cast(vf, __builtin_amdgcn_raw_buffer_load_b128(rs, boff, 0, 0));
-    }
-    // min / max of |t| bit patterns over the tile: 2^-60 <= |t| < 2^61 for the
-    // fast quotients (zeros, denormals, inf and nan all fail)
-    uint32_t mn = 0xffffffffu, mx = 0;
-#pragma unroll
-    for (int j = 0; j < KU; ++j) {
-        const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j < Ku ? j : Ku - 1));
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-            t[j][e] = t[j][e] * wk;
-            const uint32_t a = __float_as_uint(t[j][e]) & 0x7fffffffu;
-            mn = min(mn, a);
-            mx = max(mx, a);
-        }
-    }
-    const bool tile_slow = __ballot(mn < (67u << 23) || mx >= (188u << 23)) != 0;  // wave-uniform
-    for (int s = 0; s < S; ++s) {
-        const uint64_t m = __ballot((mj >> s) & 1ull);  // coalition s's clients (bit j)
-        const f32x4 cc = dv.c[s];
-        const uint32_t flags = __float_as_uint(cc.w);
-        vf acc;
-        if (ACC)
-            acc = ov[(int64_t)s * ldov + iq];
-        else
-#pragma unroll
-            for (int e = 0; e < V; ++e) acc[e] = -0.f;
-        if (!tile_slow && (flags & 3u) == 3u) {  // two-constant: q = fma(t, yh, RN(t*yl))
-            const float yh = cc.x, yl = cc.y;
-#pragma unroll
-            for (int j = 0; j < KU; ++j)
-                if ((m >> j) & 1ull) {
-                    // an empty volatile asm keeps the branch (no if-conversion into
-                    // selects, which would compute every pair)
-                    DLS_UNION_KEEP_BRANCH;
-#pragma unroll
-                    for (int e = 0; e < V; ++e)
-                        acc[e] = acc[e] + __builtin_fmaf(t[j][e], yh, t[j][e] * yl);
-                }
-        } else if (!tile_slow && (flags & 2u)) {  // Markstein
-            const float y = cc.x, b = cc.z;
-#pragma unroll
-            for (int j = 0; j < KU; ++j)
-                if ((m >> j) & 1ull) {
-                    DLS_UNION_KEEP_BRANCH;
-#pragma unroll
-                    for (int e = 0; e < V; ++e) acc[e] = acc[e] + markstein(t[j][e], b, y);
-                }
-        } else {  // zeros, denormals, huge values, inf / nan, divisors out of range
-            const float b = cc.z;
-            for (int j = 0; j < Ku; ++j)
-                if ((m >> j) & 1ull) {
-                    // dynamic j: the row again from memory (L2-warm), t recomputed
-                    const int64_t r = __builtin_amdgcn_readlane(tr, j);
-                    const float wk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
-                    const vf x = Uv[r * ldv + iq];
-#pragma unroll
-                    for (int e = 0; e < V; ++e) acc[e] = acc[e] + (x[e] * wk) / b;
-                }
-        }
-        if (i0 < PV) ov[(int64_t)s * ldov + i0] = acc;
-    }
-}
-
-
-// Double-buffered LDS form (DLS_UNION_REG == 2).  One block of kU2Waves waves per
-// CU, persistent over 256-parameter tiles (a lane owns 4).  The tile's t_j of
+// The kernel: one block of kUnionWaves waves per CU, persistent over
+// 256-parameter tiles (a lane owns 4).  The tile's t_j of
 // the <= 64 union clients live in LDS, double-buffered: while the block computes
 // tile i from one buffer, each wave's loads of tile i+1's rows are in flight, and
 // after its coalitions it turns them into t_j in the other buffer — one barrier
@@ -578,36 +255,24 @@ __global__ __launch_bounds__(kUnionRegBlock) void k_subset_union_reg(
 // and stores them after staging the next tile, so its next loads never wait
 // behind its stores.  Per membership: one ds_read_b128 of t (4 parameters), the
 // quotient (2 ops two-constant / 3 Markstein, element pairs packed) and the add.
-#ifndef DLS_UNION_SCALAR
-#define DLS_UNION_SCALAR 0
-#endif
-// f32x4 add as 4 scalar v_add_f32 (DLS_UNION_SCALAR) or 2 v_pk_add_f32
-__device__ __forceinline__ f32x4 addu(f32x4 a, f32x4 b) {
-#if DLS_UNION_SCALAR
-    f32x4 r;
-    r.x = a.x + b.x;
-    r.y = a.y + b.y;
-    r.z = a.z + b.z;
-    r.w = a.w + b.w;
-    return r;
-#else
-    return a + b;
-#endif
-}
-constexpr int kU2Waves = 16;
-constexpr int kU2KMax = 8;   // coalitions per wave (the plan caps it; 16 x 8 >= 64)
+//
+// f32x4 add as 2 v_pk_add_f32 (packed fp32 issues two lanes' elements at the
+// cost of one scalar op: tools/valu_rate_probe.hip measured 75 vs 38 T lane-op/s)
+__device__ __forceinline__ f32x4 addu(f32x4 a, f32x4 b) { return a + b; }
+constexpr int kUnionWaves = 16;
+constexpr int kUnionKMax = 8;   // coalitions per wave (the plan caps it; 16 x 8 >= 64)
 
 template <bool ACC>
-__global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
+__global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
     const f32x4 *__restrict__ Uv, int64_t ldu4, const int32_t *__restrict__ urows,
     const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku, UnionDiv dv, int S,
     int64_t P4, int64_t ntiles, f32x4 *__restrict__ out, int64_t ldo4) {
-    constexpr int W = kU2Waves, NL = kUnionChunk / kU2Waves;
+    constexpr int W = kUnionWaves, NL = kUnionChunk / kUnionWaves;
     __shared__ f32x4 ts[2][kUnionChunk * 64];                   // 2 x 64 KiB
     __shared__ uint8_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk];  // member positions, per coalition
     __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];                 // UnionDiv, per coalition
     __shared__ int lens[DLS_SUBSET_UNION_MAX];
-    __shared__ int plan[W][kU2KMax + 1];                        // [0] = count, then coalitions
+    __shared__ int plan[W][kUnionKMax + 1];                        // [0] = count, then coalitions
     __shared__ uint32_t tbad[2][W];
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;  // block-uniform
@@ -645,7 +310,7 @@ __global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
             done |= 1ull << best;
             int bw = -1;
             for (int w = 0; w < W; ++w)
-                if (plan[w][0] < kU2KMax && (bw < 0 || load[w] < load[bw])) bw = w;
+                if (plan[w][0] < kUnionKMax && (bw < 0 || load[w] < load[bw])) bw = w;
             plan[bw][1 + plan[bw][0]++] = best;
             load[bw] += lens[best] + 2;  // + the coalition's fixed cost
         }
@@ -686,21 +351,21 @@ __global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
     stage(0);
     __syncthreads();  // buffer 0 and the plan are ready
     const int nk = __builtin_amdgcn_readfirstlane(plan[wv][0]);
-    int cid[kU2KMax];
+    int cid[kUnionKMax];
 #pragma unroll
-    for (int k = 0; k < kU2KMax; ++k)
+    for (int k = 0; k < kUnionKMax; ++k)
         cid[k] = __builtin_amdgcn_readfirstlane(plan[wv][1 + (k < nk ? k : 0)]);
 #pragma unroll
-    for (int k = 0; k < kU2KMax; ++k)
+    for (int k = 0; k < kUnionKMax; ++k)
         if (k < nk) fast &= (int)((__float_as_uint(cst[cid[k]].w) & 2u) != 0);
     int b = 0;
     for (; tile < ntiles; tile += gridDim.x, b ^= 1) {
         const int64_t i0 = tile * 64 + lane;
         const int64_t iq = i0 < P4 ? i0 : P4 - 1;
         const int64_t next = tile + gridDim.x;
-        f32x4 res[kU2KMax];
+        f32x4 res[kUnionKMax];
 #pragma unroll
-        for (int k = 0; k < kU2KMax; ++k)
+        for (int k = 0; k < kUnionKMax; ++k)
             if (ACC && k < nk) res[k] = out[(int64_t)cid[k] * ldo4 + iq];
         if (next < ntiles) issue(next);  // in flight during this tile's coalitions
         uint32_t anybad = 0;
@@ -709,7 +374,7 @@ __global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
         const bool tile_fast = fast && anybad == 0;
         const char *tb = reinterpret_cast<const char *>(ts[b]) + 16 * lane;
 #pragma unroll
-        for (int k = 0; k < kU2KMax; ++k) {
+        for (int k = 0; k < kUnionKMax; ++k) {
             if (k >= nk) break;  // wave-uniform
             const int c = cid[k];
             f32x4 acc = ACC ? res[k] : f32x4{-0.f, -0.f, -0.f, -0.f};
@@ -721,26 +386,18 @@ __global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
                 return *reinterpret_cast<const f32x4 *>(tb + off);
             };
             if (__builtin_expect(tile_fast, 1)) {
-                const f32x2 y2 = f32x2{cc.x, cc.x}, l2 = f32x2{cc.y, cc.y};
-                const f32x2 b2 = f32x2{cc.z, cc.z};
+                // the coalition's constants as SGPRs (pk ops take them with op_sel,
+                // no VGPR pair copies)
+                const float cy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.x)));
+                const float cl = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.y)));
+                const float cb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.z)));
+                const f32x2 y2 = f32x2{cy, cy}, l2 = f32x2{cl, cl};
+                const f32x2 b2 = f32x2{cb, cb};
                 // the division method is decided once per coalition (two copies of
                 // the member loop), not per member
                 auto walk = [&](auto two_c) {
                     constexpr bool TWO = decltype(two_c)::value;
                     auto quot = [&](f32x4 t) {
-#if DLS_UNION_SCALAR
-                        f32x4 q;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            if constexpr (TWO) {
-                                q[e] = __builtin_fmaf(t[e], cc.x, t[e] * cc.y);
-                            } else {
-                                const float q0 = t[e] * cc.x;
-                                q[e] = __builtin_fmaf(__builtin_fmaf(-q0, cc.z, t[e]), cc.x, q0);
-                            }
-                        }
-                        return q;
-#endif
                         const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
                         f32x2 ql, qh;
                         if constexpr (TWO) {
@@ -755,22 +412,38 @@ __global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
                         }
                         return f32x4{ql.x, ql.y, qh.x, qh.y};
                     };
-                    int l = 0;
-                    if (n >= 4) {
-                        f32x4 x0 = tload(0), x1 = tload(1), x2 = tload(2), x3 = tload(3);
-                        for (; l + 8 <= n; l += 4) {
-                            const f32x4 z0 = tload(l + 4), z1 = tload(l + 5);
-                            const f32x4 z2 = tload(l + 6), z3 = tload(l + 7);
-                            const f32x4 q0 = quot(x0), q1 = quot(x1), q2 = quot(x2), q3 = quot(x3);
-                            acc = addu(addu(addu(addu(acc, q0), q1), q2), q3);
-                            x0 = z0;
-                            x1 = z1;
-                            x2 = z2;
-                            x3 = z3;
-                        }
-                        const f32x4 q0 = quot(x0), q1 = quot(x1), q2 = quot(x2), q3 = quot(x3);
+                    // groups of 4 members, ping-pong between two register sets (the
+                    // next group's t are read from LDS while this group's 4
+                    // independent quotients are computed; no register rotation)
+                    auto group = [&](const f32x4 (&x)[4]) {
+                        const f32x4 q0 = quot(x[0]), q1 = quot(x[1]), q2 = quot(x[2]),
+                                    q3 = quot(x[3]);
                         acc = addu(addu(addu(addu(acc, q0), q1), q2), q3);
-                        l += 4;
+                    };
+                    auto fetch4 = [&](int l0, f32x4 (&x)[4]) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) x[u] = tload(l0 + u);
+                    };
+                    int l = 0;
+                    const int ng = n >> 2;  // whole groups
+                    if (ng > 0) {
+                        f32x4 xa[4], xb[4];
+                        fetch4(0, xa);
+                        int g = 0;
+                        for (; g + 2 < ng; g += 2) {
+                            fetch4(4 * (g + 1), xb);
+                            group(xa);
+                            fetch4(4 * (g + 2), xa);
+                            group(xb);
+                        }
+                        if (g + 1 < ng) {
+                            fetch4(4 * (g + 1), xb);
+                            group(xa);
+                            group(xb);
+                        } else {
+                            group(xa);
+                        }
+                        l = 4 * ng;
                     }
                     for (; l < n; ++l) acc = addu(acc, quot(tload(l)));
                 };
@@ -794,8 +467,9 @@ __global__ __launch_bounds__(64 * kU2Waves) void k_subset_union2(
         }
         if (next < ntiles) stage(b ^ 1);  // the next tile's t (its loads have landed by now)
 #pragma unroll
-        for (int k = 0; k < kU2KMax; ++k)
-            if (k < nk && i0 < P4) out[(int64_t)cid[k] * ldo4 + i0] = res[k];
+        for (int k = 0; k < kUnionKMax; ++k)
+            if (k < nk && i0 < P4)
+                out[(int64_t)cid[k] * ldo4 + i0] = res[k];
         __syncthreads();  // buffer b ^ 1 is complete; buffer b free for the tile after next
     }
 }
@@ -918,88 +592,19 @@ extern "C" int dls_subset_fedavg_union_f32(const float *U, int64_t ldu, const in
     // continuing the running sums in `out` (the same fp32 additions, in order)
     for (int32_t c0 = 0; c0 < Ku; c0 += kUnionChunk) {
         const int kc = Ku - c0 < kUnionChunk ? Ku - c0 : kUnionChunk;
-#if DLS_UNION_REG == 2
-        {
-            auto launch2 = [&](auto kern) {
-                const int64_t blocks =
-                    resident_blocks(reinterpret_cast<const void *>(kern), 64 * kU2Waves, 0);
-                const dim3 grid((unsigned)(ntiles < blocks ? ntiles : blocks));
-                hipLaunchKernelGGL(kern, grid, dim3(64 * kU2Waves), 0, st,
-                                   reinterpret_cast<const f32x4 *>(U), ldu / 4, urows + c0,
-                                   uweight + c0, member + c0, kc, dv, (int)S, P4, ntiles,
-                                   reinterpret_cast<f32x4 *>(out), ldo / 4);
-            };
-            if (c0 == 0)
-                launch2(k_subset_union2<false>);
-            else  // a later chunk continues the running sums in `out`
-                launch2(k_subset_union2<true>);
-            const int rc = check_launch("dls_subset_fedavg_union_f32");
-            if (rc != DLS_OK) return rc;
-            continue;
-        }
-#elif DLS_UNION_REG
-        {
-            constexpr int V = DLS_UNION_V;
-            const int64_t PV = P / V;
-            const int64_t waves = (PV + 63) / 64;
-            const dim3 grid((unsigned)((waves + kUnionRegBlock / 64 - 1) / (kUnionRegBlock / 64)));
-            auto launch = [&](auto kern) {
-                hipLaunchKernelGGL(kern, grid, dim3(kUnionRegBlock), 0, st, U, ldu, urows + c0,
-                                   uweight + c0, member + c0, kc, dv, (int)S, PV, out, ldo);
-            };
-            // KU = the chunk's client count rounded up to 8 (V*KU registers of t)
-#define DLS_UNION_REG_KU(K_)                                          \
-    case K_ / 8:                                                      \
-        if (c0 == 0)                                                  \
-            launch(k_subset_union_reg<V, K_, false>);                 \
-        else /* a later chunk continues the running sums in `out` */ \
-            launch(k_subset_union_reg<V, K_, true>);                  \
-        break;
-            switch ((kc + 7) / 8) {
-                DLS_UNION_REG_KU(8)
-                DLS_UNION_REG_KU(16)
-                DLS_UNION_REG_KU(24)
-                DLS_UNION_REG_KU(32)
-                DLS_UNION_REG_KU(40)
-                DLS_UNION_REG_KU(48)
-                DLS_UNION_REG_KU(56)
-                DLS_UNION_REG_KU(64)
-            }
-#undef DLS_UNION_REG_KU
-            const int rc = check_launch("dls_subset_fedavg_union_f32");
-            if (rc != DLS_OK) return rc;
-            continue;
-        }
-#endif
+        const int64_t blocks = resident_blocks(reinterpret_cast<const void *>(k_subset_union<false>),
+                                               64 * kUnionWaves, 0);
+        const dim3 grid((unsigned)(ntiles < blocks ? ntiles : blocks));
         auto launch = [&](auto kern) {
-            const int64_t blocks =
-                resident_blocks(reinterpret_cast<const void *>(kern), 64 * kUnionWaves, 0);
-            const dim3 grid((unsigned)(ntiles < blocks ? ntiles : blocks));
             hipLaunchKernelGGL(kern, grid, dim3(64 * kUnionWaves), 0, st,
                                reinterpret_cast<const f32x4 *>(U), ldu / 4, urows + c0,
                                uweight + c0, member + c0, kc, dv, (int)S, P4, ntiles,
                                reinterpret_cast<f32x4 *>(out), ldo / 4);
         };
-        const int kw = (S + kUnionWaves - 1) / kUnionWaves;
-        static_assert(DLS_SUBSET_UNION_MAX == 8 * kUnionWaves, "KW instances 1..8");
-#define DLS_UNION_KW(K_)                                                 \
-    case K_:                                                             \
-        if (c0 == 0)                                                     \
-            launch(k_subset_union<K_, false>);                           \
-        else /* a later chunk continues the running sums in `out` */    \
-            launch(k_subset_union<K_, true>);                            \
-        break;
-        switch (kw) {
-            DLS_UNION_KW(1)
-            DLS_UNION_KW(2)
-            DLS_UNION_KW(3)
-            DLS_UNION_KW(4)
-            DLS_UNION_KW(5)
-            DLS_UNION_KW(6)
-            DLS_UNION_KW(7)
-            DLS_UNION_KW(8)
-        }
-#undef DLS_UNION_KW
+        if (c0 == 0)
+            launch(k_subset_union<false>);
+        else  // a later chunk continues the running sums in `out`
+            launch(k_subset_union<true>);
         const int rc = check_launch("dls_subset_fedavg_union_f32");
         if (rc != DLS_OK) return rc;
     }

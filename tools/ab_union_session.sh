@@ -1,4 +1,5 @@
 #!/bin/bash
+# Union-kernel A/B (tools/_variants libraries), after the product library's union parity tests.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
