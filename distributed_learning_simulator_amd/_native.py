@@ -49,6 +49,7 @@ _i32, _i64, _f32, _p, _u64 = (ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ct
 SIGNATURES = {
     "dls_last_error": ([], ctypes.c_char_p),
     "dls_abi_version": ([], _i32),
+    "dls_source_hash": ([], ctypes.c_char_p),
     "dls_device_count": ([], _i32),
     "dls_two_constant_division": ([_f32], _i32),
     "dls_fedavg_f32": ([_p, _i64, _p, _p, _i32, _f32, _i64, _i32, _p, _p], _i32),
@@ -117,6 +118,21 @@ def _stream(stream=None, like=None):
         dev = like.device if like is not None and like.is_cuda else None
         stream = torch.cuda.current_stream(dev)
     return ctypes.c_void_p(stream.cuda_stream)
+
+
+CSRC_HASHED = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "shapley.hip", "infer.hip",
+               "dls_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
+
+
+def source_hash():
+    """SHA-256 prefix of the library sources in this tree (the Makefile's
+    dls_source_hash recipe); compare with lib().dls_source_hash()."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in CSRC_HASHED:
+        with open(os.path.join(_HERE, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def two_constant_division(divisor):

@@ -151,6 +151,11 @@ int dls_two_constant_division(float divisor) { return dls::make_fastdiv2(divisor
 
 const char *dls_last_error(void) { return dls::g_last_error.c_str(); }
 
+#ifndef DLS_SOURCE_HASH
+#define DLS_SOURCE_HASH "unknown"
+#endif
+const char *dls_source_hash(void) { return DLS_SOURCE_HASH; }
+
 int dls_abi_version(void) { return DLS_ABI_VERSION; }
 
 int dls_device_count(void) {

@@ -80,3 +80,11 @@ def test_two_constant_division_check_without_gpu(lib):
         expect = int(np.array_equal(q, a / b32))
         assert f(b) == expect, b
     assert f(0.5) == 0  # outside the fast range: never two-constant
+
+
+def test_library_built_from_this_tree(lib):
+    """The loaded libdls_hip.so was compiled from exactly the sources in this tree
+    (the source hash the Makefile compiles in)."""
+    from distributed_learning_simulator_amd import _native
+    lib.dls_source_hash.restype = ctypes.c_char_p
+    assert lib.dls_source_hash().decode() == _native.source_hash()
