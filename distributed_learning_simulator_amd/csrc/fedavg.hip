@@ -269,7 +269,9 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
     int64_t P4, int64_t ntiles, f32x4 *__restrict__ out, int64_t ldo4) {
     constexpr int W = kUnionWaves, NL = kUnionChunk / kUnionWaves;
     __shared__ f32x4 ts[2][kUnionChunk * 64];                   // 2 x 64 KiB
-    __shared__ uint8_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk];  // member positions, per coalition
+    // member byte offsets in a t buffer (client j: j * 1 KiB), per coalition; a
+    // wave reads 4 at a time as one broadcast ds_read_b128 (no readlane per member)
+    __shared__ __attribute__((aligned(16))) uint32_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk + 4];
     __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];                 // UnionDiv, per coalition
     __shared__ int lens[DLS_SUBSET_UNION_MAX];
     __shared__ int plan[W][kUnionKMax + 1];                        // [0] = count, then coalitions
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
         if ((mj >> c) & 1ull)
             lst[c][__builtin_amdgcn_mbcnt_hi((uint32_t)(in >> 32),
                                              __builtin_amdgcn_mbcnt_lo((uint32_t)in, 0u))] =
-                (uint8_t)lane;
+                (uint32_t)lane << 10;
         if (lane == 0) {
             lens[c] = __popcll(in);
             cst[c] = dv.c[c];
@@ -380,10 +382,14 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             f32x4 acc = ACC ? res[k] : f32x4{-0.f, -0.f, -0.f, -0.f};
             const f32x4 cc = cst[c];
             const int n = lens[c];
-            const uint32_t vl = (uint32_t)lst[c][lane] << 10;  // lane l: member l's offset
+            const uint32_t *ml = lst[c];
             auto tload = [&](int l) {
-                const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)vl, l);
-                return *reinterpret_cast<const f32x4 *>(tb + off);
+                return *reinterpret_cast<const f32x4 *>(tb + ml[l]);
+            };
+            auto tload4 = [&](int l, f32x4 (&x)[4]) {  // members l..l+3 (l % 4 == 0)
+                const u32x4 o = *reinterpret_cast<const u32x4 *>(ml + l);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f32x4 *>(tb + o[u]);
             };
             if (__builtin_expect(tile_fast, 1)) {
                 // the coalition's constants as SGPRs (pk ops take them with op_sel,
@@ -420,10 +426,7 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
                                     q3 = quot(x[3]);
                         acc = addu(addu(addu(addu(acc, q0), q1), q2), q3);
                     };
-                    auto fetch4 = [&](int l0, f32x4 (&x)[4]) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) x[u] = tload(l0 + u);
-                    };
+                    auto fetch4 = [&](int l0, f32x4 (&x)[4]) { tload4(l0, x); };
                     int l = 0;
                     const int ng = n >> 2;  // whole groups
                     if (ng > 0) {
