@@ -171,6 +171,40 @@ def bench_fedavg(args, dev, rank, world, scaling="weak"):
                            "params": layout.numel, "padded_row": P}
 
 
+def bench_fedavg_bitexact_sharded(args, dev, world, rank):
+    """Config 2 strong scaling through ShardedFedServer(exchange="alltoall"): the
+    bit-exact multi-GPU round (parameter slices per rank, one all-to-all of the
+    client rows, the reference-order kernel over all clients per slice, one
+    all-gather); args.clients clients in total, dealt worker_id % world."""
+    from distributed_learning_simulator_amd.distributed import ShardedFedServer
+    shapes = resnet18_cifar()
+    server = ShardedFedServer(tester=None, worker_number=args.clients, synchronous=True,
+                              device=dev, exchange="alltoall")
+    g = torch.Generator(device=dev).manual_seed(SEED + 11 + rank)
+    for wid in server.local_worker_ids:
+        d = {k: torch.randn(sh, generator=g, device=dev) * 0.05 for k, sh in shapes}
+        server.parameters[wid] = (100 + 9 * wid, d)
+    ids = list(server.parameters.keys())
+
+    def step(a=None, b=None):
+        if a is not None:
+            a.record()
+        server.get_subset_model(ids)
+        if b is not None:
+            b.record()
+
+    wall, _ = timed_launches(step, max(3, args.steps // 4), 2, dist.barrier)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item()) / max(3, args.steps // 4) * 1e3
+    numel = sum(math.prod(sh) for _, sh in shapes)
+    del server
+    return {"config": f"FedAvg of {args.clients} ResNet-18 updates in total over {world} GPUs, "
+                      "bit-exact for any rank count (all-to-all of parameter slices + all-gather)",
+            "value": round(args.clients * numel * 4 / (ms / 1e3) / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(ms, 4), "scaling": "strong"}
+
+
 # ------------------------------------------------------------ components
 def bench_fedavg_k1000(args, dev):
     """North-star scale: FedAvg of 1000 ResNet-18-sized updates (44.7 GB in HBM)."""
@@ -737,6 +771,8 @@ def main():
                  lambda *a: dict(zip(("value", "ms_per_step", "roofline", "config"),
                                      bench_fedavg(args, dev, rank, world, other)),
                                  scaling=other, unit="GB/s")),
+                ("fedavg_bitexact_sharded",
+                 lambda *a: bench_fedavg_bitexact_sharded(args, dev, world, rank)),
                 ("sign_vote_sharded", lambda *a: bench_sign_sharded(args, dev, world, rank)),
                 ("fed_quant_sharded", lambda *a: bench_quant_sharded(args, dev, world, rank)),
                 ("shapley_evals", lambda *a: bench_shapley_evals(args, dev, world, rank))]

@@ -14,6 +14,9 @@ collective combines the ranks:
   transfer of chunk c overlaps the reduction of chunk c+1.  Reference-order
   within a shard, cross-rank sums in RCCL order: normwise ~1e-7 vs the exact
   mean (north-star tolerance 1e-6), not bit-exact.
+  ``ShardedFedServer(exchange="alltoall")`` is the bit-exact alternative:
+  parameter slices per rank, one all-to-all of the client rows, the
+  reference-order kernel over all clients on each slice, one all-gather.
 * sign vote: int32 vote counts per rank, SUM all-reduce, then sign on every
   rank — bit-exact for any number of ranks.
 
@@ -102,16 +105,92 @@ class _ShardedMixin:
         return len(self.local_worker_ids)
 
 
-class ShardedFedServer(_ShardedMixin, FedServer):
-    """FedServer whose round is spread over all ranks (one process per GPU)."""
+def slice_bounds(P, world):
+    """Parameter slices of a P-element row (P a multiple of 64) for ``world`` ranks:
+    contiguous, multiples of 64 elements, sizes within 64 of each other."""
+    units = P // 64
+    return [units * r // world * 64 for r in range(world)] + [P]
 
-    def __init__(self, group=None, chunks=3, **kwargs):
+
+class ShardedFedServer(_ShardedMixin, FedServer):
+    """FedServer whose round is spread over all ranks (one process per GPU).
+
+    ``exchange="allreduce"`` (default): each rank reduces its own clients with the
+    global N, then a chunked fp32 SUM all-reduce — one P-element exchange,
+    normwise ~1e-7 of the exact mean.  ``exchange="alltoall"``: bit-exact for any
+    number of ranks: every rank owns a parameter slice, one
+    all-to-all moves every client's slice to its owner, each rank runs the
+    reference-order kernel over ALL K clients (worker-id order, the order a
+    single server sees when the clients report in id order) on its slice, and an
+    all-gather assembles the mean — bits identical to one FedServer, at the cost
+    of moving (world-1)/world of the client rows instead of one P-vector."""
+
+    def __init__(self, group=None, chunks=3, exchange="allreduce", **kwargs):
+        if exchange not in ("allreduce", "alltoall"):
+            raise ValueError(f"exchange must be 'allreduce' or 'alltoall', not {exchange!r}")
+        self.exchange = exchange
         self._init_shard(kwargs["worker_number"], group, chunks)
         super().__init__(**kwargs)
+
+    def _bitexact_mean(self, ids):
+        """exchange="alltoall": the mean of every rank's clients, bit-exact."""
+        store = self.parameters.store
+        P, dev, world = store.layout.P, self.device, self.world_size
+        kmax = max(1, -(-self.worker_number // world))  # >= any rank's local clients
+        meta = torch.full((kmax, 2), -1, dtype=torch.int64, device=dev)
+        for j, wid in enumerate(ids):
+            meta[j, 0] = wid
+            meta[j, 1] = self.parameters.n_of(wid)
+        metas = torch.empty((world * kmax, 2), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(metas, meta, group=self.group)
+        metas = metas.view(world, kmax, 2)
+        bounds = slice_bounds(P, world)
+        L = max(bounds[r + 1] - bounds[r] for r in range(world))
+        send = torch.zeros((world, kmax, L), dtype=torch.float32, device=dev)
+        for j, wid in enumerate(ids):
+            row = store.row(self.parameters.row_of(wid))
+            for d in range(world):
+                send[d, j, : bounds[d + 1] - bounds[d]].copy_(row[bounds[d]:bounds[d + 1]])
+        # gloo moves host tensors only (single-GPU test runs): stage through the host
+        host = dist.get_backend(self.group) == "gloo" and send.is_cuda
+        if host:
+            r = torch.empty(send.shape, dtype=send.dtype)
+            dist.all_to_all_single(r, send.cpu(), group=self.group)
+            recv = r.to(dev)
+        else:
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.group)
+        # recv[s, j]: my slice of rank s's j-th client; all K clients in worker-id order
+        order = sorted((int(wid), int(n), s * kmax + j)
+                       for s, m in enumerate(metas.tolist()) for j, (wid, n) in enumerate(m)
+                       if wid >= 0)
+        total = sum(n for _, n, _ in order)
+        mine = bounds[self.rank + 1] - bounds[self.rank]
+        part = torch.zeros(L, dtype=torch.float32, device=dev)
+        from .aggregation import _f32, _i32
+        from .servers.fed_server import _MODES
+        _native.fedavg(recv.view(world * kmax, L), _i32([r for _, _, r in order], dev),
+                       _f32([n for _, n, _ in order], dev), float(total), mine, part,
+                       mode=_MODES[self.aggregation_mode])
+        if host:
+            ph = torch.empty(world * L, dtype=torch.float32)
+            dist.all_gather_into_tensor(ph, part.cpu(), group=self.group)
+            parts = ph.to(dev).view(world, L)
+        else:
+            parts = torch.empty(world * L, dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(parts, part, group=self.group)
+            parts = parts.view(world, L)
+        out = torch.empty(P, dtype=torch.float32, device=dev)
+        for r in range(world):
+            out[bounds[r]:bounds[r + 1]].copy_(parts[r, : bounds[r + 1] - bounds[r]])
+        return out
 
     def get_subset_model(self, client_subset):
         if not client_subset:
             return self.prev_model
+        if self.exchange == "alltoall":
+            ids = [i for i in client_subset if i in self.parameters]
+            return self.parameters.store.layout.views(self._bitexact_mean(ids))
         ids = [i for i in client_subset if i in self.parameters]
         ns = [self.parameters.n_of(i) for i in ids]
         total = global_sample_count(ns, self.device, self.group)

@@ -63,6 +63,28 @@ def _fedavg_worker(rank, world, port, outq):
     dist.destroy_process_group()
 
 
+def _fedavg_bitexact_worker(rank, world, port, outq):
+    _init(rank, world, port)
+    from distributed_learning_simulator_amd.distributed import ShardedFedServer
+    z = G.load("fedavg.npz")
+    case = G.meta(z)[1]
+    k, layout, K = case["key"], case["layout"], case["K"]
+    U, n = z[f"{k}_U"], z[f"{k}_n"]
+    server = ShardedFedServer(tester=None, worker_number=K, synchronous=True,
+                              device=torch.device("cpu"), exchange="alltoall")
+    q = server.worker_data_queue
+    for w in server.local_worker_ids:
+        q.get_result(consumer=w, timeout=30)
+    for wid in reversed(server.local_worker_ids):  # arrival order must not matter
+        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
+        q.add_task((wid, int(n[wid]), d))
+    for w in server.local_worker_ids:
+        res = q.get_result(consumer=w, timeout=30)
+    assert len(q._results) == 0
+    outq.put((rank, np.concatenate([res[nm].reshape(-1).numpy() for nm, _ in layout])))
+    dist.destroy_process_group()
+
+
 def _sign_worker(rank, world, port, outq):
     _init(rank, world, port)
     from distributed_learning_simulator_amd.distributed import ShardedSignSGDServer
@@ -134,6 +156,22 @@ def test_sharded_fedavg_two_ranks():
     assert np.linalg.norm(got - ex) / np.linalg.norm(ex) < 1e-6
     ref = z[f"{k}_full"]  # single-process reference result: same within normwise 1e-6
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-6
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fedavg_alltoall_bit_exact(world):
+    """exchange="alltoall": bits identical to one server aggregating all K clients
+    in worker-id order, for any number of ranks."""
+    z = G.load("fedavg.npz")
+    case = G.meta(z)[1]
+    k = case["key"]
+    out = _spawn(_fedavg_bitexact_worker, world)
+    from oracle import _c
+    U = z[f"{k}_U"]
+    ref = _c.fedavg_ref(U, [int(x) for x in z[f"{k}_n"]], list(range(case["K"])))
+    P = ref.size
+    for _, got in out:
+        assert np.array_equal(got[:P].view(np.uint32), ref.view(np.uint32))
 
 
 def test_sharded_sign_vote_two_ranks_bit_exact():

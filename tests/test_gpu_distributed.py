@@ -55,6 +55,18 @@ def _worker(rank, world, port, backend, outq):
         fed.append(np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout]))
     assert np.array_equal(fed[0].view(np.uint32), fed[1].view(np.uint32))
     out["fed"] = fed[0]
+    # bit-exact exchange (parameter slices, all-to-all + all-gather)
+    sx = ShardedFedServer(tester=None, worker_number=K, synchronous=True, exchange="alltoall")
+    qx = sx.worker_data_queue
+    for w in sx.local_worker_ids:
+        qx.get_result(consumer=w, timeout=60)
+    for wid in reversed(sx.local_worker_ids):
+        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
+        qx.add_task((wid, int(n[wid]), d))
+    for w in sx.local_worker_ids:
+        res = qx.get_result(consumer=w, timeout=60)
+    assert len(qx._results) == 0
+    out["fed_exact"] = np.concatenate([res[nm].reshape(-1).cpu().numpy() for nm, _ in layout])
     # sign vote
     zs = G.load("sign_vote.npz")
     cs = G.meta(zs)[1]
@@ -116,3 +128,9 @@ def test_sharded_servers_two_ranks(backend):
         zq = G.load("dequant.npz")
         assert np.linalg.norm(outs[r]["quant"] - zq["agg"]) / np.linalg.norm(zq["agg"]) < 1e-6
     assert np.array_equal(outs[0]["fed"].view(np.uint32), outs[1]["fed"].view(np.uint32))
+    # exchange="alltoall": bits of one server aggregating every client in worker-id order
+    from oracle import _c
+    case = G.meta(z)[1]
+    ref = _c.fedavg_ref(z[f"{k}_U"], [int(x) for x in z[f"{k}_n"]], list(range(case["K"])))
+    for r in (0, 1):
+        assert np.array_equal(outs[r]["fed_exact"][: ref.size].view(np.uint32), ref.view(np.uint32))
