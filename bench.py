@@ -74,15 +74,33 @@ def timed_launches(fn, steps, warmup, sync_all=None):
     return wall, [a.elapsed_time(b) for a, b in ev]
 
 
-def load_traffic(key):
-    """HBM bytes per launch of this workload's kernel from the committed rocprofv3
-    PMC passes (profiles/pmc_traffic.json, tools/pmc_summary.py), if present."""
+def load_pmc(key):
+    """This workload's entry of the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, tools/pmc_traffic.py), or {}."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(key, {})
     except (OSError, ValueError):
+        return {}
+
+
+def load_traffic(key):
+    """HBM bytes per launch of this workload's kernel from the PMC passes, if present."""
+    return load_pmc(key).get("hbm_bytes_per_launch")
+
+
+def valu_issue(kernel, key):
+    """The VALU issue roof from counters: the fraction of the 1024 SIMDs' cycles
+    their VALU was busy while this workload's kernels ran (4 x SQ_ACTIVE_INST_VALU
+    / (1024 x GRBM_GUI_ACTIVE / 8), profiles/pmc_traffic.json); 1.0 = every SIMD
+    issuing a VALU instruction every 4 cycles.  None without the SQ pass."""
+    f = load_pmc(key).get("valu_busy_frac")
+    if f is None:
         return None
+    return {"kernel": kernel, "bound": "valu_issue", "achieved": round(f, 4), "peak": 1.0,
+            "unit": "VALU-busy fraction of SIMD cycles", "frac": round(f, 4),
+            "source": "rocprofv3 SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE (profiles/pmc_traffic.json)"}
 
 
 def roofline(kernel, bytes_per_launch, kernel_ms, bound="hbm", flops_per_launch=None, key=None):
@@ -274,6 +292,7 @@ def bench_sign(args, dev):
         "ms_per_step": round(ms, 4),
         "roofline": roofline("dls_sign_vote", bytes_per_launch, kms, key="sign_vote"),
         "pack": roofline("dls_sign_pack_f32", 16 * (P * 4 + W * 8), pkms, key="sign_pack"),
+        "valu_issue": valu_issue("dls_sign_vote", "sign_vote"),
     }
 
 
@@ -408,6 +427,7 @@ def bench_quant(args, dev, K=100, shapes=None, model="VGG-16", key="fed_quant"):
         "roofline": roofline("dls_dequant_fedavg", bytes_per_launch, kms, key=key),
         "valu_roof": roofline("dls_dequant_fedavg", bytes_per_launch, kms, bound="valu",
                               flops_per_launch=valu_ops),
+        "valu_issue": valu_issue("dls_dequant_fedavg", key),
     }
 
 
@@ -483,6 +503,7 @@ def bench_shapley_exact(args, dev):
                              key="shapley_exact"),
         "valu_roof": roofline("dls_subset_fedavg_union_f32", bytes_per_launch, kms, bound="valu",
                               flops_per_launch=valu_ops),
+        "valu_issue": valu_issue("dls_subset_fedavg_union_f32", "shapley_exact"),
         "per_coalition_kernel_ms": round(sum(kms_pc) / len(kms_pc), 4),
     }
 

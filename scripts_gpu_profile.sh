@@ -3,7 +3,7 @@
 #   1. kernel trace + stats of bench.py's headline (FedAvg, config 2) alone;
 #   2. kernel trace + stats of every bench.py workload (no CPU baseline);
 #   3. per workload, separate PMC passes for FETCH_SIZE and WRITE_SIZE (they cannot
-#      share a pass on gfx950) and one of 8 SQ counters, each over exactly
+#      share a pass on gfx950) and one of 8 SQ counters + GRBM_GUI_ACTIVE, each over exactly
 #      N + 1 C-ABI calls of the product library (tools/ab_bench.py --only-run).
 # Only the stats CSVs and the counter rows of this library's kernels are kept,
 # under gpurun_out/prof_<tag>/; tools/pmc_traffic.py summarises them.
@@ -39,7 +39,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/
     python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --evals 2 > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.log" || exit $?
 keep_stats trace
 for W in $WLS; do
-    for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD"; do
+    for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"; do
         P="pmc_${W}_$(echo $C | cut -d' ' -f1)"
         DLS_VARIANTS="$LIBDIR" timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$RAW/$P" -o run -- \
             python3 "$ROOT/tools/ab_bench.py" --workloads "$W" --only-run --launches 3 > "$OUT/$P.log" 2>&1 || exit $?

@@ -5,11 +5,17 @@
   key (read by bench.py as roofline.traffic), from the FETCH_SIZE / WRITE_SIZE
   passes: every pass makes exactly 3 calls (tools/ab_bench.py --only-run
   --launches 3), so bytes per call = the sum over all of
-  this library's kernels in the pass / 4 (one call may launch several kernels:
+  this library's kernels in the pass / 3 (one call may launch several kernels:
   FedAvg's one-generation pieces, fed_quant's tile groups).
   Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are KiB; on
   gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads,
   so hbm_read = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B stores.
+  With the SQ pass it also carries `valu_busy_frac`: the fraction of the
+  SIMDs' issue cycles the VALU was busy, 4 * SQ_ACTIVE_INST_VALU (quad-cycles,
+  summed over waves) / (1024 SIMDs * GRBM_GUI_ACTIVE / 8) (GRBM_GUI_ACTIVE is
+  the sum over the 8 XCDs of each dispatch's busy cycles; rocprofv3 serialises
+  dispatches while counting, so kernels that run concurrently in the product
+  are counted one after another here).
 * profiles/<tag>_pmc_summary.txt: the same plus the SQ counter ratios.
 
     python tools/pmc_traffic.py <tag>
@@ -23,6 +29,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CALLS = 3
+SIMDS, XCDS = 1024, 8  # MI355X: 256 CUs x 4 SIMDs, 8 XCDs
 KEYS = {"fedavg": "headline", "fedavg1k": "fedavg_k1000", "vote_sign": "sign_vote",
         "pack": "sign_pack", "quant": "fed_quant", "quant_r18": "fed_quant_k1000",
         "union": "shapley_exact", "gemm": "shapley_gemm", "bn_act": "bn_act"}
@@ -62,6 +69,12 @@ def main(tag):
             lines.append("    of SQ_WAVE_CYCLES: " + ", ".join(
                 f"{k}={sq[k] / wc:.3f}" for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")
                 if k in sq))
+            out_json[key]["sq_per_call"] = {k: v / CALLS for k, v in sorted(sq.items())}
+            if sq.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in sq:
+                busy = 4 * sq["SQ_ACTIVE_INST_VALU"] / (SIMDS * sq["GRBM_GUI_ACTIVE"] / XCDS)
+                out_json[key]["valu_busy_frac"] = busy
+                lines.append(f"    VALU busy {busy:.3f} of the SIMDs' cycles "
+                             f"(4 x SQ_ACTIVE_INST_VALU / (1024 x GRBM_GUI_ACTIVE / 8))")
         except OSError:
             pass
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fo:
