@@ -1,6 +1,7 @@
 """Quantized FedAvg worker (reference: workers/fed_quant_worker.py:15-69).
 
-The reference trains with the absent library's QAT, sends
+The reference trains with the absent library's QAT
+(``QuantizationAwareTraining(replace_layer=False)``, :19-20), sends
 ``qat.get_quantized_parameters()`` to a ``self.server`` attribute that does not
 exist (D2, so it never runs), logs the pickle-size compression ratio (``model_util.get_data_serialization_size``) and loads
 the server's answer.  This worker keeps the evident protocol on the task
@@ -10,6 +11,14 @@ per output channel, symmetric int8 — torch's default QAT weight scheme
 segment min/max + qparams + quantize kernels, sends
 ``(worker_id, n, {name: (int8 weight, scale[C], zero_point[C]) | fp32})``
 and loads the dequantized aggregate the ``FedQuantServer`` broadcasts.
+
+Quantization-aware training (``qat=True``, the reference's default): while the
+worker trains, every weight tensor (dim >= 2) enters the forward pass as its
+per-channel symmetric int8 fake-quantization ``fl(q * scale)`` with the qparams
+of the current weights (the same device kernels as the export, so the model the
+worker optimises is the one it sends), and its gradient passes straight through
+(STE).  The absent library's QAT observers and layer handling are not
+reproduced: parity unpinned.
 """
 import logging
 
@@ -43,11 +52,61 @@ def quantize_per_channel_symmetric(w):
     return q.reshape(w.shape), scale, zp
 
 
+class _StraightThrough(torch.autograd.Function):
+    """Forward: the fake-quantized weight; backward: the gradient unchanged."""
+
+    @staticmethod
+    def forward(ctx, w, fq):
+        return fq
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+@torch.no_grad()
+def fake_quantize_per_channel_symmetric(w):
+    q, scale, _ = quantize_per_channel_symmetric(w)
+    return q.float() * scale.view(-1, *([1] * (w.dim() - 1)))
+
+
+class WeightFakeQuant:
+    """QAT hooks: each module owning a weight Parameter with dim >= 2 (conv,
+    linear) sees ``_StraightThrough(w, fake_quant(w))`` as its weight during its
+    forward; the Parameter itself (and the optimizer's reference) is unchanged."""
+
+    def __init__(self, model):
+        self.handles = []
+        for mod in model.modules():
+            w = mod._parameters.get("weight")
+            if isinstance(w, torch.nn.Parameter) and w.dim() >= 2:
+                self.handles.append(mod.register_forward_pre_hook(self._pre))
+                self.handles.append(mod.register_forward_hook(self._post))
+
+    @staticmethod
+    def _pre(mod, _args):
+        w = mod._parameters["weight"]
+        mod._qat_weight = w
+        mod._parameters["weight"] = _StraightThrough.apply(w, fake_quantize_per_channel_symmetric(w))
+
+    @staticmethod
+    def _post(mod, _args, _out):
+        mod._parameters["weight"] = mod._qat_weight
+        del mod._qat_weight
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+        self.handles = []
+
+
 class FedQuantWorker(Worker):
     def __init__(self, **kwargs):
         worker_round = kwargs.pop("round")
+        qat = kwargs.pop("qat", True)
         super().__init__(**kwargs)
         self.round = worker_round
+        self.qat = WeightFakeQuant(self.trainer.model) if qat else None
         self.trainer.add_named_callback(ModelExecutorCallbackPoint.AFTER_EXECUTE, "quantization",
                                         self.__send_parameters)
         # serialized sizes, as the reference (workers/fed_quant_worker.py:28-30,43)

@@ -405,3 +405,45 @@ def test_dequant_fedavg_lane_tiles_resnet_shapes(K):
                 for k, v in p.items()} for p in payloads]
     ref = oquant.dequant_fedavg(clients, n, order, layout)
     assert same_bits(flat(out, layout), ref)
+
+
+def test_qat_weight_fake_quant_ste():
+    """The fed_quant worker's quantization-aware training (ref
+    workers/fed_quant_worker.py:19-20): conv / linear weights enter the forward
+    pass as fl(q * scale) with torch's per-channel symmetric int8 qparams of the
+    current weights, the gradient reaches the fp32 Parameter unchanged (STE), and
+    the Parameter itself is restored after every forward.  The absent library's
+    QAT details are not reproduced (parity unpinned); the fake-quantized weight
+    is pinned bit-exact to torch.quantize_per_channel's ints times the scale."""
+    import torch.nn.functional as F
+    from distributed_learning_simulator_amd.workers.fed_quant_worker import (
+        WeightFakeQuant, fake_quantize_per_channel_symmetric)
+    g = torch.Generator().manual_seed(7)
+    conv = torch.nn.Conv2d(3, 8, 3)
+    lin = torch.nn.Linear(8 * 6 * 6, 10)
+    model = torch.nn.Sequential(conv, torch.nn.ReLU(), torch.nn.Flatten(), lin).to(dev)
+    for w in (conv.weight, lin.weight):
+        obs = torch.ao.quantization.PerChannelMinMaxObserver(
+            ch_axis=0, dtype=torch.qint8, qscheme=torch.per_channel_symmetric)
+        wc = w.detach().cpu()
+        obs(wc)
+        sc, zp = obs.calculate_qparams()
+        qi = torch.quantize_per_channel(wc, sc.double(), zp, 0, torch.qint8).int_repr().float()
+        ref = qi * sc.float().view(-1, *([1] * (wc.dim() - 1)))
+        assert torch.equal(fake_quantize_per_channel_symmetric(w).cpu(), ref)
+    x = torch.randn((4, 3, 8, 8), generator=g).to(dev)
+    hooks = WeightFakeQuant(model)
+    y = model(x)
+    assert isinstance(conv.weight, torch.nn.Parameter) and isinstance(lin.weight, torch.nn.Parameter)
+    y.square().sum().backward()
+    # the same forward with the fake-quantized weights as leaves
+    cw = fake_quantize_per_channel_symmetric(conv.weight).requires_grad_()
+    lw = fake_quantize_per_channel_symmetric(lin.weight).requires_grad_()
+    y2 = F.linear(F.relu(F.conv2d(x, cw, conv.bias)).flatten(1), lw, lin.bias)
+    y2.square().sum().backward()
+    assert torch.allclose(y, y2, rtol=0, atol=1e-6)
+    assert torch.allclose(conv.weight.grad, cw.grad, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(lin.weight.grad, lw.grad, rtol=1e-5, atol=1e-6)
+    hooks.remove()
+    plain = F.linear(F.relu(F.conv2d(x, conv.weight, conv.bias)).flatten(1), lin.weight, lin.bias)
+    assert torch.allclose(model(x), plain, rtol=0, atol=1e-6)
