@@ -199,7 +199,7 @@ def setup(dev, want=()):
     uth = (ctypes.c_float * len(ut))(*ut)
     W["union"] = (lambda L: L.dls_subset_fedavg_union_f32(ptr(U), P, ptr(ur), ptr(uwt), ptr(um), 50,
                                                           uth, 50, P, ptr(uo), P, stream()),
-                  100 * P * 4)
+                  100 * P * 4, uo)
     off, fr, fw, ft = [0], [], [], []
     for sub in subs:
         fr += sub
@@ -237,6 +237,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--only-run", action="store_true", help="just launch (rocprofv3 target)")
+    ap.add_argument("--check", action="store_true",
+                    help="workloads that name their output: every variant's bits equal the first's")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -247,7 +249,20 @@ def main():
     W = setup(dev, args.workloads.split(","))
     res = {}
     for wl in args.workloads.split(","):
-        fn, nbytes = W[wl]
+        fn, nbytes = W[wl][:2]
+        if args.check and len(W[wl]) > 2:
+            ref = None
+            for name, L in libs.items():
+                W[wl][2].fill_(float("nan"))
+                assert fn(L) == 0
+                torch.cuda.synchronize()
+                got = W[wl][2].clone()
+                if ref is None:
+                    ref = got
+                else:
+                    same = torch.equal(got.view(torch.int32), ref.view(torch.int32))
+                    print(wl, "check", name, "bit-identical" if same else "DIFFERS", flush=True)
+                    assert same, (wl, name)
         if args.only_run:  # a profiler target: the first variant only, launches back to back
             L = next(iter(libs.values()))
             for _ in range(args.launches):
