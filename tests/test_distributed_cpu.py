@@ -158,10 +158,10 @@ def test_sharded_fedavg_two_ranks():
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-6
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_fedavg_alltoall_bit_exact(world):
     """exchange="alltoall": bits identical to one server aggregating all K clients
-    in worker-id order, for any number of ranks."""
+    in worker-id order, for any number of ranks (8: the node the driver scales to)."""
     z = G.load("fedavg.npz")
     case = G.meta(z)[1]
     k = case["key"]
