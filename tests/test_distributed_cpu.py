@@ -1,4 +1,4 @@
-"""world_size-2 ``gloo`` tests of the sharded (multi-GPU) servers' host logic on CPU.
+"""Multi-rank ``gloo`` tests (2, 3 and 8 ranks) of the sharded (multi-GPU) servers' host logic on CPU.
 
 Kernels are replaced by numpy doubles (tests/cpu_doubles.py); what is tested is
 the sharding (worker_id % world), the global sample count, the chunked
@@ -174,9 +174,10 @@ def test_sharded_fedavg_alltoall_bit_exact(world):
         assert np.array_equal(got[:P].view(np.uint32), ref.view(np.uint32))
 
 
-def test_sharded_sign_vote_two_ranks_bit_exact():
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_sign_vote_bit_exact(world):
     z = G.load("sign_vote.npz")
-    out = _spawn(_sign_worker)
+    out = _spawn(_sign_worker, world)
     for _, v in out:
         assert np.array_equal(v.view(np.uint32), z["c1_vote"].view(np.uint32))
 
