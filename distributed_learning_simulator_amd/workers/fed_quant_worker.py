@@ -85,7 +85,10 @@ class WeightFakeQuant:
 
     @staticmethod
     def _pre(mod, _args):
-        w = mod._parameters["weight"]
+        # a forward that raised never reached _post: its Parameter is still parked
+        w = mod.__dict__.get("_qat_weight")
+        if w is None:
+            w = mod._parameters["weight"]
         mod._qat_weight = w
         mod._parameters["weight"] = _StraightThrough.apply(w, fake_quantize_per_channel_symmetric(w))
 
