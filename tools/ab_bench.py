@@ -85,7 +85,8 @@ def setup(dev, want=()):
                                                None, stream()), 1000 * Wd * 8 + 2 * P * 4)
         vp = torch.empty(Wd, dtype=torch.int64, device=dev)
         W["vote_sign"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, None, ptr(so),
-                                                    ptr(vp), stream()), 1000 * Wd * 8 + P * 4 + Wd * 8)
+                                                    ptr(vp), stream()), 1000 * Wd * 8 + P * 4 + Wd * 8,
+                          so)
         X = torch.sign(torch.randn((16, P), generator=g, device=dev))
         pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
         W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
