@@ -183,7 +183,7 @@ def setup(dev, want=()):
                 lambda L, tdev=tdev, tt=tt, nft=nft: L.dls_dequant_fedavg(
                     ptr(tdev), len(tt), nfast_arg(L, nft), ptr(sr.Q), sr.Q.stride(0), ptr(sr.F),
                     sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
-                    ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb)
+                    ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb, qo18)
         qs.LANE_TILE = saved
         W["quant_r18"] = W[f"quant_r18_l{saved // 1024}"]
     # Shapley default path: 50 coalitions (members with p = 1/2) over 50 clients,
