@@ -570,19 +570,27 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     """Config 5b: Shapley utility evaluations through ShapleyValueServer.evaluate_subsets
     (batched bit-exact subset models + ResNet-18 test-set inference; on N ranks the
     coalitions are dealt round-robin and the utilities all-reduced).  Weak scaling:
-    args.evals coalitions per GPU."""
+    args.evals coalitions per GPU.  Timed with the tester's default module forward
+    (the value) and again with its opt-in fused batch-norm pass (``fused_eval``)."""
     server = _shapley_eval_server(args, dev)
     coal = _shapley_coalitions(50, (args.evals + 2) * world, SEED + 7)
-    server.evaluate_subsets(coal[: 2 * world])  # MIOpen kernel selection, warm caches
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    vals = server.evaluate_subsets(coal[2 * world:])
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        el = _max_over_ranks(el, dev)
+
+    def timed(fused):
+        server.tester.fused_eval = fused
+        server.evaluate_subsets(coal[: 2 * world])  # MIOpen kernel selection, warm caches
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        vals = server.evaluate_subsets(coal[2 * world:])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            el = _max_over_ranks(el, dev)
+        return el, vals
+
+    el, vals = timed(False)
+    el_f, vals_f = timed(True)
     n = len(coal) - 2 * world
     del server
     torch.cuda.empty_cache()
@@ -593,6 +601,12 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
             "value": round(n / el, 3), "unit": "subset-evals/s (all GPUs)",
             "ms_per_eval_per_gpu": round(el / n * world * 1e3, 2),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
+            "fused_eval": {"value": round(n / el_f, 3), "unit": "subset-evals/s (all GPUs)",
+                           "ms_per_eval_per_gpu": round(el_f / n * world * 1e3, 2),
+                           "max_utility_diff": round(max(abs(a - b) for a, b in zip(vals, vals_f)),
+                                                     6),
+                           "note": "opt-in Inferencer(fused_eval=True): eval batch norm + "
+                                   "residual + ReLU as one HIP pass (dls_bn_act_nhwc_f32)"},
             "bn_act": bn}
 
 

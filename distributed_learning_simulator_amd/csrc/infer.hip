@@ -35,12 +35,13 @@ __global__ __launch_bounds__(kBnBlock) void k_bn_fold(const float *__restrict__ 
 
 // FIXED: C/4 divides the grid's thread count, so a thread's channel group never
 // changes and its (alpha, beta) stay in registers.
+// y may alias x (the in-place call of the fused forward) or r: no __restrict__ on
+// them; every element is read before its own store and by the same thread.
 template <bool FIXED, bool RES, bool RELU>
-__global__ __launch_bounds__(kBnBlock) void k_bn_act(const f32x4 *__restrict__ x, int64_t n4,
-                                                     int C4, const f32x4 *__restrict__ alpha,
+__global__ __launch_bounds__(kBnBlock) void k_bn_act(const f32x4 *x, int64_t n4, int C4,
+                                                     const f32x4 *__restrict__ alpha,
                                                      const f32x4 *__restrict__ beta,
-                                                     const f32x4 *__restrict__ r,
-                                                     f32x4 *__restrict__ y) {
+                                                     const f32x4 *r, f32x4 *y) {
     const int64_t stride = (int64_t)gridDim.x * kBnBlock;
     int64_t i = (int64_t)blockIdx.x * kBnBlock + threadIdx.x;
     f32x4 a = {}, bb = {};

@@ -23,6 +23,8 @@ collective combines the ranks:
 Client-to-rank placement mirrors the reference's ``worker_id % ngpu``
 (simulator.py:68).
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -107,9 +109,11 @@ class _ShardedMixin:
 
 def slice_bounds(P, world):
     """Parameter slices of a P-element row (P a multiple of 64) for ``world`` ranks:
-    contiguous, multiples of 64 elements, sizes within 64 of each other."""
-    units = P // 64
-    return [units * r // world * 64 for r in range(world)] + [P]
+    contiguous, equal lengths L (a multiple of 64; the last slices are short or
+    empty when P is not a multiple of L), so the slice means all-gather straight
+    into one [world * L] output."""
+    L = -(-P // (64 * world)) * 64
+    return [min(P, r * L) for r in range(world)] + [P]
 
 
 class ShardedFedServer(_ShardedMixin, FedServer):
@@ -118,72 +122,117 @@ class ShardedFedServer(_ShardedMixin, FedServer):
     ``exchange="allreduce"`` (default): each rank reduces its own clients with the
     global N, then a chunked fp32 SUM all-reduce — one P-element exchange,
     normwise ~1e-7 of the exact mean.  ``exchange="alltoall"``: bit-exact for any
-    number of ranks: every rank owns a parameter slice, one
-    all-to-all moves every client's slice to its owner, each rank runs the
-    reference-order kernel over ALL K clients (worker-id order, the order a
-    single server sees when the clients report in id order) on its slice, and an
-    all-gather assembles the mean — bits identical to one FedServer, at the cost
-    of moving (world-1)/world of the client rows instead of one P-vector."""
+    number of ranks: every rank owns a parameter slice, every
+    client's slice moves from its rank's store row straight to its owner
+    (point-to-point sends batched into one RCCL group, no staging copy), each
+    rank runs the reference-order kernel over ALL K clients on its slice, and an
+    all-gather assembles the mean — bits identical to one FedServer that saw the
+    clients in the same order, at the cost of moving (world-1)/world of the
+    client rows instead of one P-vector.
 
-    def __init__(self, group=None, chunks=3, exchange="allreduce", **kwargs):
+    ``order`` (alltoall only) is the client order of the sum: ``"arrival"`` (the
+    reference's: ``self.parameters.keys()`` in insertion order,
+    servers/fed_server.py:69-73,81) merges the ranks' arrivals by the
+    node-wide monotonic clock at which each update reached its rank's queue
+    thread (ties by worker id); ``"worker_id"`` sorts by id."""
+
+    def __init__(self, group=None, chunks=3, exchange="allreduce", order="arrival", **kwargs):
         if exchange not in ("allreduce", "alltoall"):
             raise ValueError(f"exchange must be 'allreduce' or 'alltoall', not {exchange!r}")
+        if order not in ("arrival", "worker_id"):
+            raise ValueError(f"order must be 'arrival' or 'worker_id', not {order!r}")
         self.exchange = exchange
+        self.order = order
+        self._arrival = {}
+        self._clock = time.monotonic_ns  # system-wide on Linux: comparable across ranks
         self._init_shard(kwargs["worker_number"], group, chunks)
         super().__init__(**kwargs)
+
+    def _process_worker_data(self, data, __):
+        wid = data[0]
+        if wid not in self._arrival:  # a re-sent update keeps its first place, like a dict key
+            self._arrival[wid] = self._clock()
+        result = super()._process_worker_data(data, __)
+        if result is not None:  # the round is over: its clients' updates were cleared
+            self._arrival.clear()
+        return result
+
+    def _global_order(self, ids):
+        """[(worker_id, n, home rank)] of every rank's clients in summation order."""
+        dev, world = self.device, self.world_size
+        kmax = max(1, -(-self.worker_number // world))  # >= any rank's local clients
+        meta = [[int(wid), self.parameters.n_of(wid), self._arrival.get(wid, 0)] for wid in ids]
+        meta += [[-1, 0, 0]] * (kmax - len(meta))
+        meta = torch.tensor(meta, dtype=torch.int64).to(dev)  # one host -> device copy
+        metas = torch.empty((world * kmax, 3), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(metas, meta, group=self.group)
+        entries = [(t, wid, n, i // kmax) for i, (wid, n, t) in enumerate(metas.tolist())
+                   if wid >= 0]
+        if self.order == "worker_id":
+            entries.sort(key=lambda e: e[1])
+        else:
+            entries.sort(key=lambda e: (e[0], e[1]))
+        return [(wid, n, home) for _, wid, n, home in entries]
 
     def _bitexact_mean(self, ids):
         """exchange="alltoall": the mean of every rank's clients, bit-exact."""
         store = self.parameters.store
-        P, dev, world = store.layout.P, self.device, self.world_size
-        kmax = max(1, -(-self.worker_number // world))  # >= any rank's local clients
-        meta = torch.full((kmax, 2), -1, dtype=torch.int64, device=dev)
-        for j, wid in enumerate(ids):
-            meta[j, 0] = wid
-            meta[j, 1] = self.parameters.n_of(wid)
-        metas = torch.empty((world * kmax, 2), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(metas, meta, group=self.group)
-        metas = metas.view(world, kmax, 2)
+        P, dev, world, me = store.layout.P, self.device, self.world_size, self.rank
+        order = self._global_order(ids)
         bounds = slice_bounds(P, world)
-        L = max(bounds[r + 1] - bounds[r] for r in range(world))
-        send = torch.zeros((world, kmax, L), dtype=torch.float32, device=dev)
-        for j, wid in enumerate(ids):
-            row = store.row(self.parameters.row_of(wid))
-            for d in range(world):
-                send[d, j, : bounds[d + 1] - bounds[d]].copy_(row[bounds[d]:bounds[d + 1]])
-        # gloo moves host tensors only (single-GPU test runs): stage through the host
-        host = dist.get_backend(self.group) == "gloo" and send.is_cuda
-        if host:
-            r = torch.empty(send.shape, dtype=send.dtype)
-            dist.all_to_all_single(r, send.cpu(), group=self.group)
-            recv = r.to(dev)
-        else:
-            recv = torch.empty_like(send)
-            dist.all_to_all_single(recv, send, group=self.group)
-        # recv[s, j]: my slice of rank s's j-th client; all K clients in worker-id order
-        order = sorted((int(wid), int(n), s * kmax + j)
-                       for s, m in enumerate(metas.tolist()) for j, (wid, n) in enumerate(m)
-                       if wid >= 0)
+        L = bounds[1] - bounds[0]
+        mine = bounds[me + 1] - bounds[me]
+        # recv[i]: my slice of the i-th client of the summation order; my own
+        # clients' slices are copied out of the store (1/world of my rows), every
+        # other rank's arrive point-to-point from its store rows
+        recv = torch.empty((len(order), max(mine, 4)), dtype=torch.float32, device=dev)
+        staged = dist.get_backend(self.group) == "gloo" and recv.is_cuda  # gloo: host tensors
+        ops, landing = [], []
+        for i, (wid, _, home) in enumerate(order):
+            if home == me:
+                row = store.row(self.parameters.row_of(wid))
+                recv[i, :mine].copy_(row[bounds[me]:bounds[me] + mine])
+                for d in range(world):
+                    n_d = bounds[d + 1] - bounds[d]
+                    if d == me or n_d == 0:
+                        continue
+                    src = row[bounds[d]:bounds[d + 1]]
+                    ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src,
+                                          self._peer(d)))
+            elif mine > 0:
+                dst = recv[i, :mine]
+                if staged:
+                    host = torch.empty(mine, dtype=torch.float32)
+                    landing.append((dst, host))
+                    dst = host
+                ops.append(dist.P2POp(dist.irecv, dst, self._peer(home)))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        for dst, host in landing:
+            dst.copy_(host)
         total = sum(n for _, n, _ in order)
-        mine = bounds[self.rank + 1] - bounds[self.rank]
         part = torch.zeros(L, dtype=torch.float32, device=dev)
-        from .aggregation import _f32, _i32
-        from .servers.fed_server import _MODES
-        _native.fedavg(recv.view(world * kmax, L), _i32([r for _, _, r in order], dev),
-                       _f32([n for _, n, _ in order], dev), float(total), mine, part,
-                       mode=_MODES[self.aggregation_mode])
-        if host:
-            ph = torch.empty(world * L, dtype=torch.float32)
-            dist.all_gather_into_tensor(ph, part.cpu(), group=self.group)
-            parts = ph.to(dev).view(world, L)
+        if mine > 0:  # a rank whose slice is empty (P < 64 * world) only joins the gather
+            from .aggregation import _f32
+            from .servers.fed_server import _MODES
+            _native.fedavg(recv, torch.arange(len(order), dtype=torch.int32, device=dev),
+                           _f32([n for _, n, _ in order], dev), float(total), mine, part,
+                           mode=_MODES[self.aggregation_mode])
+        out = torch.empty(world * L, dtype=torch.float32, device=dev)
+        if staged:
+            oh = torch.empty(world * L, dtype=torch.float32)
+            dist.all_gather_into_tensor(oh, part.cpu(), group=self.group)
+            out.copy_(oh)
         else:
-            parts = torch.empty(world * L, dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(parts, part, group=self.group)
-            parts = parts.view(world, L)
-        out = torch.empty(P, dtype=torch.float32, device=dev)
-        for r in range(world):
-            out[bounds[r]:bounds[r + 1]].copy_(parts[r, : bounds[r + 1] - bounds[r]])
-        return out
+            dist.all_gather_into_tensor(out, part, group=self.group)
+        return out[:P]
+
+    def _peer(self, rank):
+        """Global rank of ``rank`` in self.group (P2P ops take global ranks)."""
+        if self.group is None:
+            return rank
+        return dist.get_global_rank(self.group, rank)
 
     def get_subset_model(self, client_subset):
         if not client_subset:

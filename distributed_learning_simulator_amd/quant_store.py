@@ -100,7 +100,7 @@ class QuantLayout:
         return True
 
     def tiles(self):
-        """(table, nfast): wave tiles; nfast = counts of the 8 grouped kinds at the
+        """(table, nfast): wave tiles; nfast = counts of the 10 grouped kinds at the
         head of the table (dls_hip.h DLS_QTILE_GROUPS), then the general tiles.
 
         * one-channel tiles (groups 0-3: 4, 3, 2, 1 KiB slices): int tensors whose

@@ -71,36 +71,37 @@ def fake_quantize_per_channel_symmetric(w):
 
 
 class WeightFakeQuant:
-    """QAT hooks: each module owning a weight Parameter with dim >= 2 (conv,
-    linear) sees ``_StraightThrough(w, fake_quant(w))`` as its weight during its
-    forward; the Parameter itself (and the optimizer's reference) is unchanged."""
+    """QAT: each module owning a weight Parameter with dim >= 2 (conv, linear)
+    sees ``_StraightThrough(w, fake_quant(w))`` as its weight during its forward;
+    the Parameter itself (and the optimizer's reference) is unchanged, and it is
+    back in place when the forward returns or raises (the module's forward is
+    wrapped in try/finally, so named_parameters() / state_dict() / .to() never
+    see the fake-quantized tensor)."""
 
     def __init__(self, model):
-        self.handles = []
+        self.modules = []
         for mod in model.modules():
             w = mod._parameters.get("weight")
             if isinstance(w, torch.nn.Parameter) and w.dim() >= 2:
-                self.handles.append(mod.register_forward_pre_hook(self._pre))
-                self.handles.append(mod.register_forward_hook(self._post))
+                mod.forward = self._wrap(mod, mod.forward)
+                self.modules.append(mod)
 
     @staticmethod
-    def _pre(mod, _args):
-        # a forward that raised never reached _post: its Parameter is still parked
-        w = mod.__dict__.get("_qat_weight")
-        if w is None:
+    def _wrap(mod, forward):
+        def fake_quant_forward(*args, **kwargs):
             w = mod._parameters["weight"]
-        mod._qat_weight = w
-        mod._parameters["weight"] = _StraightThrough.apply(w, fake_quantize_per_channel_symmetric(w))
-
-    @staticmethod
-    def _post(mod, _args, _out):
-        mod._parameters["weight"] = mod._qat_weight
-        del mod._qat_weight
+            mod._parameters["weight"] = _StraightThrough.apply(
+                w, fake_quantize_per_channel_symmetric(w))
+            try:
+                return forward(*args, **kwargs)
+            finally:
+                mod._parameters["weight"] = w
+        return fake_quant_forward
 
     def remove(self):
-        for h in self.handles:
-            h.remove()
-        self.handles = []
+        for mod in self.modules:
+            del mod.forward  # the instance attribute: the class's forward again
+        self.modules = []
 
 
 class FedQuantWorker(Worker):

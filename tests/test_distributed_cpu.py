@@ -71,17 +71,48 @@ def _fedavg_bitexact_worker(rank, world, port, outq):
     k, layout, K = case["key"], case["layout"], case["K"]
     U, n = z[f"{k}_U"], z[f"{k}_n"]
     server = ShardedFedServer(tester=None, worker_number=K, synchronous=True,
-                              device=torch.device("cpu"), exchange="alltoall")
+                              device=torch.device("cpu"), exchange="alltoall", order="worker_id")
     q = server.worker_data_queue
     for w in server.local_worker_ids:
         q.get_result(consumer=w, timeout=30)
-    for wid in reversed(server.local_worker_ids):  # arrival order must not matter
+    for wid in reversed(server.local_worker_ids):  # order="worker_id": arrivals do not matter
         d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
         q.add_task((wid, int(n[wid]), d))
     for w in server.local_worker_ids:
         res = q.get_result(consumer=w, timeout=30)
     assert len(q._results) == 0
     outq.put((rank, np.concatenate([res[nm].reshape(-1).numpy() for nm, _ in layout])))
+    dist.destroy_process_group()
+
+
+def _fedavg_arrival_worker(rank, world, port, outq):
+    """order="arrival": clients report in a fixed global sequence; the server's
+    arrival clock is replaced by the client's position in it (the ranks' queue
+    threads would otherwise stamp the node-wide monotonic clock), so the merged
+    order must be that sequence — the order one reference server would have seen."""
+    _init(rank, world, port)
+    from distributed_learning_simulator_amd.distributed import ShardedFedServer
+    z = G.load("fedavg.npz")
+    case = G.meta(z)[1]
+    k, layout, K = case["key"], case["layout"], case["K"]
+    U, n = z[f"{k}_U"], z[f"{k}_n"]
+    server = ShardedFedServer(tester=None, worker_number=K, synchronous=True,
+                              device=torch.device("cpu"), exchange="alltoall")
+    q = server.worker_data_queue
+    for w in server.local_worker_ids:
+        q.get_result(consumer=w, timeout=30)
+    seq = np.random.RandomState(7).permutation(K).tolist()
+    for rnd in range(2):  # the second round re-stamps every arrival
+        order = seq if rnd == 0 else seq[::-1]
+        for t, wid in enumerate(order):
+            if wid in server.local_worker_ids:
+                server._clock = lambda t=t: 1000 * rnd + t
+                d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(U[wid], layout).items()}
+                q.add_task((wid, int(n[wid]), d))
+        for w in server.local_worker_ids:
+            res = q.get_result(consumer=w, timeout=30)
+        outq.put((rank, rnd, order, np.concatenate([res[nm].reshape(-1).numpy()
+                                                     for nm, _ in layout])))
     dist.destroy_process_group()
 
 
@@ -172,6 +203,37 @@ def test_sharded_fedavg_alltoall_bit_exact(world):
     P = ref.size
     for _, got in out:
         assert np.array_equal(got[:P].view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fedavg_alltoall_arrival_order(world):
+    """exchange="alltoall", order="arrival": bits identical to one server summing
+    the clients in the order they arrived over all ranks (ref
+    servers/fed_server.py:69-73,81: self.parameters.keys() in insertion order)."""
+    z = G.load("fedavg.npz")
+    case = G.meta(z)[1]
+    k = case["key"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fedavg_arrival_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(2 * world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    from oracle import _c
+    U = z[f"{k}_U"]
+    ns = [int(x) for x in z[f"{k}_n"]]
+    for _, _, order, got in out:
+        ref = _c.fedavg_ref(U, ns, order)
+        assert np.array_equal(got[:ref.size].view(np.uint32), ref.view(np.uint32))
+    # the two rounds' orders give different bits (the order is really followed)
+    r0 = next(g for _, rnd, _, g in out if rnd == 0)
+    r1 = next(g for _, rnd, _, g in out if rnd == 1)
+    assert not np.array_equal(r0.view(np.uint32), r1.view(np.uint32))
 
 
 @pytest.mark.parametrize("world", [2, 8])

@@ -56,7 +56,8 @@ def _worker(rank, world, port, backend, outq):
     assert np.array_equal(fed[0].view(np.uint32), fed[1].view(np.uint32))
     out["fed"] = fed[0]
     # bit-exact exchange (parameter slices, all-to-all + all-gather)
-    sx = ShardedFedServer(tester=None, worker_number=K, synchronous=True, exchange="alltoall")
+    sx = ShardedFedServer(tester=None, worker_number=K, synchronous=True, exchange="alltoall",
+                          order="worker_id")
     qx = sx.worker_data_queue
     for w in sx.local_worker_ids:
         qx.get_result(consumer=w, timeout=60)

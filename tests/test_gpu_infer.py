@@ -95,9 +95,15 @@ def test_resnet18_fused_eval_matches_torch():
     top2 = torch.topk(ref, 2, dim=1).values
     clear = (top2[:, 0] - top2[:, 1]) > 1e-3 * top2[:, 0].abs().clamp_min(1e-6)
     assert torch.equal(got.argmax(1)[clear], ref.argmax(1)[clear])
-    # the Inferencer takes the fused path on the GPU; accuracy as torch's forward
-    inf = Inferencer(model, (X, y), batch_size=256, device=dev)
+    # fused_eval=True: the Inferencer takes the fused path on the GPU; accuracy as
+    # torch's forward up to near-tied predictions
+    inf = Inferencer(model, (X, y), batch_size=256, device=dev, fused_eval=True)
     _, acc, _ = inf.inference()
     ref_acc = float((ref.argmax(1).cpu() == y).float().mean())
     assert abs(acc - ref_acc) <= 2 / 600
     assert np.isfinite(float(inf.loss_metric.value))
+    # the default is the module's own forward: the accuracy of torch's eval forward
+    plain = Inferencer(model, (X, y), batch_size=256, device=dev)
+    assert plain.fused_eval is False
+    _, acc0, _ = plain.inference()
+    assert acc0 == ref_acc

@@ -250,18 +250,11 @@ def test_dequant_fedavg_division_methods(total, two):
     assert same_bits(flat(out, layout), ref)
 
 
-def test_dequant_fedavg_full_vgg16_sampled_channels():
-    """BASELINE config 4 at full size: 100 clients x VGG-16 (13.8 GB of int8 in
-    HBM, 138,357,544 parameters) through the production tile table.  Every
-    output element of three channels per int tensor (first, last, one random:
-    one-channel 4 KiB / 1 KiB tiles and the general kernel's conv rows) and of
-    every fp32 tensor is checked bit-exactly against the oracle run on those
-    channels alone, clients in a shuffled reference order."""
-    import math
-    from distributed_learning_simulator_amd.model_shapes import vgg16
+def _full_model_store(shapes, K, seed):
+    """K synthetic int8 payloads of a full model in a device store, filled the
+    way bench.py fills it: raw int8 bytes, per-channel symmetric scales (zero
+    point 0, the torch QAT default), fp32 1-d tensors."""
     from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
-    K = 100
-    shapes = vgg16()
     template = {}
     for name, s in shapes:
         if len(s) >= 2:
@@ -271,24 +264,28 @@ def test_dequant_fedavg_full_vgg16_sampled_channels():
         else:
             template[name] = torch.zeros(s)
     st = QuantizedClientStore(template, dev, capacity=K)
-    g = torch.Generator(device=dev).manual_seed(4)
+    g = torch.Generator(device=dev).manual_seed(seed)
     st.Q.random_(0, 256, generator=g)  # raw int8 bytes
     st.F.normal_(generator=g)
     st.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
     st.sz[..., 1].zero_()  # symmetric int8 (torch QAT default)
-    gc = torch.Generator().manual_seed(4)
-    n = torch.randint(100, 1001, (K,), generator=gc).tolist()
-    order = torch.randperm(K, generator=gc).tolist()
-    out = st.layout.views(st.fedavg(order, [n[r] for r in order]))
-    torch.cuda.synchronize()
+    return st
 
+
+def _check_sampled_channels(st, shapes, out, n, order, gc, extra_channels=None):
+    """Every output element of three channels per int tensor (first, last, one
+    random, plus ``extra_channels[name]``) and of every fp32 tensor, bit-exact vs
+    the oracle run on those channels alone in the same client order."""
+    import math
+    K = st.capacity
     ql = st.qlayout
     clients = [dict() for _ in range(K)]
     layout, got = [], []
     for i, (name, s) in enumerate(shapes):
         if ql.kinds[i]:
             C, rl, src, cb = ql.channels[i], ql.row_len[i], ql.src[i], ql.chan_base[i]
-            cs = sorted({0, C - 1, int(torch.randint(0, C, (1,), generator=gc))})
+            cs = sorted({0, C - 1, int(torch.randint(0, C, (1,), generator=gc))}
+                        | set((extra_channels or {}).get(name, ())))
             q = torch.stack([st.Q[:, src + c * rl:src + (c + 1) * rl] for c in cs], 1)
             q = q.cpu().numpy().view(np.int8)  # [K, len(cs), rl]
             sc = st.sz[[cb + c for c in cs], :, 0].t().cpu().numpy().astype(np.float64)
@@ -306,6 +303,58 @@ def test_dequant_fedavg_full_vgg16_sampled_channels():
             got.append(out[name].reshape(-1).cpu().numpy())
     ref = oquant.dequant_fedavg(clients, n, order, layout)
     assert same_bits(np.concatenate(got), ref)
+
+
+def test_dequant_fedavg_full_resnet18_k1000_sampled_channels():
+    """The north-star instance bench.py times (fed_quant_k1000): 1000 clients x
+    ResNet-18 int8 (11.2 GB in HBM) through the production tile table — every
+    tile group the store builds (multi-channel lane tiles, fp32 tiles, the small
+    int tiles of the 27-element first-conv rows), all 16 of the kernels'
+    64-client chunks (15 full + one of 40), one client whose scale leaves the
+    fast-division range on one channel of every int tensor (the per-client IEEE
+    fallback of the lane and small-int kernels), clients in a shuffled reference order.  Sampled channels of
+    every int tensor (including the fallback channel) and every fp32 tensor are
+    bit-exact vs the oracle (ref servers/fed_quant_server.py:25-33 +
+    servers/fed_server.py:44-66)."""
+    from distributed_learning_simulator_amd.model_shapes import resnet18_cifar
+    K = 1000
+    shapes = resnet18_cifar()
+    st = _full_model_store(shapes, K, seed=18)
+    nf = st.nfast
+    assert sum(nf[4:8]) > 0 and nf[8] > 0 and nf[9] > 0, nf  # lane, fp32, small int groups
+    ql = st.qlayout
+    gc = torch.Generator().manual_seed(18)
+    bad_row = 613  # this client's channel 5 of every int tensor takes the IEEE path
+    extra = {}
+    for i, (name, s) in enumerate(shapes):
+        if ql.kinds[i]:
+            c = min(5, ql.channels[i] - 1)
+            st.sz[ql.chan_base[i] + c, bad_row, 0] = 3e30
+            extra[name] = (c,)
+    n = torch.randint(100, 1001, (K,), generator=gc).tolist()
+    order = torch.randperm(K, generator=gc).tolist()
+    out = st.layout.views(st.fedavg(order, [n[r] for r in order]))
+    torch.cuda.synchronize()
+    _check_sampled_channels(st, shapes, out, n, order, gc, extra)
+
+
+def test_dequant_fedavg_full_vgg16_sampled_channels():
+    """BASELINE config 4 at full size: 100 clients x VGG-16 (13.8 GB of int8 in
+    HBM, 138,357,544 parameters) through the production tile table.  Every
+    output element of three channels per int tensor (first, last, one random:
+    one-channel 4 KiB / 1 KiB tiles and the general kernel's conv rows) and of
+    every fp32 tensor is checked bit-exactly against the oracle run on those
+    channels alone, clients in a shuffled reference order."""
+    from distributed_learning_simulator_amd.model_shapes import vgg16
+    K = 100
+    shapes = vgg16()
+    st = _full_model_store(shapes, K, seed=4)
+    gc = torch.Generator().manual_seed(4)
+    n = torch.randint(100, 1001, (K,), generator=gc).tolist()
+    order = torch.randperm(K, generator=gc).tolist()
+    out = st.layout.views(st.fedavg(order, [n[r] for r in order]))
+    torch.cuda.synchronize()
+    _check_sampled_channels(st, shapes, out, n, order, gc)
 
 
 def test_int8_symmetric_per_channel_quantize_golden():
@@ -444,6 +493,13 @@ def test_qat_weight_fake_quant_ste():
     assert torch.allclose(y, y2, rtol=0, atol=1e-6)
     assert torch.allclose(conv.weight.grad, cw.grad, rtol=1e-5, atol=1e-6)
     assert torch.allclose(lin.weight.grad, lw.grad, rtol=1e-5, atol=1e-6)
+    # a forward that raises leaves the Parameters in place (the hooks
+    # used to park them until the next forward)
+    with pytest.raises(RuntimeError):
+        model(torch.randn((4, 5, 8, 8), device=dev))  # wrong channel count
+    names = dict(model.named_parameters())
+    assert names["0.weight"] is conv.weight and names["3.weight"] is lin.weight
+    assert all(isinstance(p, torch.nn.Parameter) and p.is_leaf for p in names.values())
     hooks.remove()
     plain = F.linear(F.relu(F.conv2d(x, conv.weight, conv.bias)).flatten(1), lin.weight, lin.bias)
     assert torch.allclose(model(x), plain, rtol=0, atol=1e-6)

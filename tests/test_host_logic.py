@@ -320,6 +320,43 @@ def test_shapley_host_logic_config5_scale(doubles, tag, tmp_path):
         assert (tmp_path / "metric_1").read_bytes() == case["metric_pickle"]
 
 
+@pytest.mark.parametrize("tag", ["gtg_50_4", "multiround_12"])
+def test_shapley_host_logic_config5_gemm_method(doubles, tag, tmp_path):
+    """subset_method="gemm" host logic at config 5's client count with the GEMM
+    double (fp64 product rounded to fp32, not the reference's op order): SV
+    within 1e-5 and the identical client ranking (north_star tolerance)."""
+    from distributed_learning_simulator_amd.servers.GTG_shapley_value_server import \
+        GTGShapleyValueServer
+    from distributed_learning_simulator_amd.servers.multiround_shapley_value_server import \
+        MultiRoundShapleyValueServer
+    case = next(c for c in G.shapley_large_cases() if c["tag"] == tag)
+    layout = [(nm, tuple(s)) for nm, s in case["layout"]]
+    K = case["K"]
+    target = case["target"]
+    gtg = tag.startswith("gtg")
+    cls = GTGShapleyValueServer if gtg else MultiRoundShapleyValueServer
+    kw = {} if gtg else {"metric_dir": str(tmp_path)}
+    server = cls(tester=None, worker_number=K, synchronous=True, device=CPU,
+                 subset_method="gemm", **kw)
+    server._set_prev_model(G.split(torch.tensor(case["prev"]), layout))
+
+    def util(model, metric_type="acc"):
+        v = np.concatenate([np.asarray(model[nm], np.float64).reshape(-1) for nm, _ in layout])
+        d = v - target
+        return float(1.0 / (1.0 + float(np.dot(d, d)) / case["scale"]))
+
+    server.get_metric = util
+    np.random.seed(case["seed"])
+    for i in range(K):
+        d = {nm: torch.from_numpy(v.copy()) for nm, v in G.split(case["U"][i], layout).items()}
+        server.worker_data_queue.add_task((i, int(case["n"][i]), d))
+    sv = server.shapley_values[1]
+    ref = {int(k): v for k, v in case["sv"].items()}
+    for k, v in ref.items():
+        assert abs(float(sv[k]) - v) <= 1e-5, k
+    assert sorted(ref, key=ref.get) == sorted(sv, key=lambda k: float(sv[k]))
+
+
 def test_data_serialization_size_matches_pickle():
     """The compression-ratio sizes (ref servers/fed_quant_server.py:41-42,
     workers/fed_quant_worker.py:28-30,43) are len(pickle.dumps(payload)) of the
