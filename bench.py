@@ -437,6 +437,73 @@ def bench_quant_k1000(args, dev):
                        key="fed_quant_k1000")
 
 
+CONFIG1 = dict(worker_number=10, rounds=5, train_size=60000, test_size=10000, epoch=1,
+               batch_size=64, learning_rate=0.01)
+
+
+def bench_config1(args, dev):
+    """BASELINE config 1 end to end on the GPU: FedAvg, 10 workers (threads, as
+    simulator.py:59-69), LeNet-5 on MNIST-shaped synthetic data (60,000 training /
+    10,000 test images), 5 rounds, through simulator.run (the drop-in factory,
+    queue, FedWorker, FedServer with the dls_fedavg_f32 aggregation and the
+    tester).  Per-round wall time = time between consecutive aggregations (round 1
+    from the start of the run, so it carries the workers' start-up)."""
+    from distributed_learning_simulator_amd import simulator
+    from distributed_learning_simulator_amd.servers.fed_server import FedServer
+    c = CONFIG1
+    cfg = simulator.get_config([
+        "--distributed_algorithm", "fed", "--worker_number", str(c["worker_number"]),
+        "--round", str(c["rounds"]), "--dataset_name", "MNIST", "--model_name", "LeNet5",
+        "--epoch", str(c["epoch"]), "--batch_size", str(c["batch_size"]),
+        "--learning_rate", str(c["learning_rate"]), "--train_size", str(c["train_size"]),
+        "--test_size", str(c["test_size"]), "--log_dir", "", "--log_level", "WARNING"])
+    stamps, agg_s = [], []
+    orig = FedServer.get_subset_model
+
+    def timed_subset(self, subset):
+        t0 = time.perf_counter()
+        out = orig(self, subset)
+        torch.cuda.synchronize()
+        agg_s.append(time.perf_counter() - t0)
+        stamps.append(time.perf_counter())
+        return out
+
+    FedServer.get_subset_model = timed_subset
+    try:
+        t0 = time.perf_counter()
+        server = simulator.run(cfg)
+        wall = time.perf_counter() - t0
+    finally:
+        FedServer.get_subset_model = orig
+    rounds = [b - a for a, b in zip([t0] + stamps[:-1], stamps)]
+    acc = server.get_metric(server.prev_model)
+    return {"config": "FedAvg, 10 workers, LeNet-5 on MNIST-shaped synthetic data (60k train / "
+                      "10k test), 5 rounds, simulator.run on 1 GPU (worker threads + server)",
+            "value": round(sum(rounds[1:]) / max(1, len(rounds) - 1), 4),
+            "unit": "s per round (rounds 2-5)", "higher_is_better": False,
+            "round_s": [round(r, 4) for r in rounds], "wall_s": round(wall, 3),
+            "aggregation_ms": [round(a * 1e3, 3) for a in agg_s],
+            "rounds": server.round, "test_accuracy": acc}
+
+
+def cpu_config1(args, threads):
+    """BASELINE config 1 on the host cores: the reference's FedAvg simulator loop
+    restated (oracle/simulator.py), same model, data shapes, split and
+    hyper-parameters as bench_config1; bounded to about args.cpu_seconds."""
+    from distributed_learning_simulator_amd.models import LeNet5, synthetic_classification
+    from oracle.simulator import run_fedavg_cpu  # test infrastructure, timed only
+    c = CONFIG1
+    train = synthetic_classification(c["train_size"], (1, 32, 32), seed=0)
+    test = synthetic_classification(c["test_size"], (1, 32, 32), seed=1)
+    times, accs = run_fedavg_cpu(LeNet5, train, test, c["worker_number"], c["rounds"],
+                                 epoch=c["epoch"], batch_size=c["batch_size"],
+                                 learning_rate=c["learning_rate"], max_seconds=args.cpu_seconds)
+    return {"value": round(sum(times) / len(times), 4), "unit": "s per round",
+            "higher_is_better": False, "cores": threads, "kind": "port",
+            "sample": f"{len(times)} of {c['rounds']} rounds (10 workers x 6,000 images, LeNet-5)",
+            "round_s": [round(t, 3) for t in times], "test_accuracy": accs[-1]}
+
+
 def _shapley_coalitions(K, S, seed):
     """S coalitions of K clients, members with probability 1/2 (client 0 always),
     as sorted tuples (how the Shapley servers pass them)."""
@@ -665,12 +732,14 @@ def cpu_baseline(args):
                       if l.startswith("Model name")), "")
     except Exception:
         pass
+    config1 = cpu_config1(args, threads)
     return {"value": round(Kc * P * 4 / per / 1e9, 3), "unit": "GB/s", "cores": threads,
             "kind": "port",
             "sample": f"{Kc} ResNet-18 client dicts (fp32, 62 tensors), reference torch op "
                       f"sequence, {reps} reps in {el:.1f}s",
             "cpu_model": model or platform.processor(), "ms_per_aggregation": round(per * 1e3, 2),
-            "components": {"shapley_evals": shapley, **cpu_components(args, threads)}}
+            "components": {"shapley_evals": shapley, **cpu_components(args, threads),
+                           "config1": config1}}
 
 
 def cpu_shapley_eval(args, clients, n, threads):
@@ -773,7 +842,7 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1")
     ap.add_argument("--only", default="", help="comma list: headline,fedavg_other_scaling,"
                     "fedavg_k1000,sign_vote,fed_quant,fed_quant_k1000,shapley_exact,shapley_gemm,"
-                    "shapley_evals,sign_vote_sharded,fed_quant_sharded")
+                    "shapley_evals,sign_vote_sharded,fed_quant_sharded,config1")
     ap.add_argument("--cpu-clients", type=int, default=100,
                     help="CPU baseline: clients of the config-2 aggregation (full K = 100)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -821,7 +890,8 @@ def main():
     if not args.quick and rank == 0:
         local_parts = [("fedavg_k1000", bench_fedavg_k1000), ("sign_vote", bench_sign),
                        ("fed_quant", bench_quant), ("fed_quant_k1000", bench_quant_k1000),
-                       ("shapley_exact", bench_shapley_exact), ("shapley_gemm", bench_shapley_gemm)]
+                       ("shapley_exact", bench_shapley_exact), ("shapley_gemm", bench_shapley_gemm),
+                       ("config1", bench_config1)]
         if world == 1:
             local_parts.append(("shapley_evals", bench_shapley_evals))
         for name, fn in local_parts:

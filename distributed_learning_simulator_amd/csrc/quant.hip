@@ -820,7 +820,10 @@ __global__ __launch_bounds__(kBlock) void k_dequant_small(const dls_qtile *__res
                 step(o);
             });
     }
-    if (e0 < lenpad) {
+    // tiles start 64-aligned in the output row: lanes up to the tensor's 64-element
+    // row padding store, so the padding reads as zero (the re-quantization's
+    // segment min / max spans it)
+    if (e0 < ((t.len + 63) & ~63)) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[e] = e0 + e < t.len ? acc[e] : 0.f;  // keep padding zero
         *reinterpret_cast<f32x4 *>(out + t.dst + e0) = acc;

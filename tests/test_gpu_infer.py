@@ -103,7 +103,10 @@ def test_resnet18_fused_eval_matches_torch():
     assert abs(acc - ref_acc) <= 2 / 600
     assert np.isfinite(float(inf.loss_metric.value))
     # the default is the module's own forward: the accuracy of torch's eval forward
+    # over the same batches (MIOpen may pick other algorithms for other batch sizes)
     plain = Inferencer(model, (X, y), batch_size=256, device=dev)
     assert plain.fused_eval is False
     _, acc0, _ = plain.inference()
-    assert acc0 == ref_acc
+    with torch.no_grad():
+        pred = torch.cat([model(xb[i:i + 256]).argmax(1) for i in range(0, xb.shape[0], 256)])
+    assert acc0 == float((pred.cpu() == y).float().mean())

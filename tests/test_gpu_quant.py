@@ -19,6 +19,16 @@ def same_bits(a, b):
         a.view(np.uint32)[~nan], b.view(np.uint32)[~nan])
 
 
+def assert_padding_zero(layout, full):
+    """Every tile kind writes its tensor's 64-element row padding as zero (the
+    re-quantization's per-tensor min / max spans it), whatever the buffer held."""
+    f = full.cpu().numpy()
+    ends = [o + m for o, m in zip(layout.offsets, layout.numels)]
+    starts = layout.offsets[1:] + [layout.P]
+    for a, b in zip(ends, starts):
+        assert np.array_equal(f[a:b].view(np.uint32), np.zeros(b - a, np.uint32)), (a, b)
+
+
 def golden_payloads():
     z = G.load("dequant.npz")
     case = G.meta(z)[0]
@@ -98,7 +108,9 @@ def test_dequant_fedavg_channel_shapes(row_len):
         r = store.acquire()
         store.write(r, p)
         rows.append(r)
-    out = store.layout.views(store.fedavg(rows, n))
+    full = torch.full((store.layout.P,), float("nan"), device=dev)  # stale memory
+    out = store.layout.views(store.fedavg(rows, n, out=full))
+    assert_padding_zero(store.layout, full)
     layout = [("a", (C, row_len)), ("bias", (C,)), ("b", (C + 1, row_len))]
     clients = [{k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy())
                 for k, v in p.items()} for p in payloads]
@@ -447,7 +459,10 @@ def test_dequant_fedavg_lane_tiles_resnet_shapes(K):
         store.write(r, p)
         rows.append(r)
     order = list(torch.randperm(K, generator=g).tolist())
-    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order]))
+    full = torch.full((store.layout.P,), float("nan"), device=dev)
+    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order],
+                                          out=full))
+    assert_padding_zero(store.layout, full)
     layout = [(k, tuple(v[0].shape) if isinstance(v, tuple) else tuple(v.shape))
               for k, v in payloads[0].items()]
     clients = [{k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy())
