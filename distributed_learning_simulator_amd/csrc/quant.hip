@@ -19,10 +19,10 @@ constexpr int kBlock = 256;
 constexpr int kQuantU = 2;      // clients per batch (1 KiB tiles); two batches in flight per lane
 constexpr int kQuantUG = 1;     // clients per batch on multi-KiB tiles
 constexpr int kQuantSched = 2;  // element pairs between scheduling barriers
-#ifndef DLS_LANE_U
-#define DLS_LANE_U 2
+#ifndef DLS_LANE_US
+#define DLS_LANE_US 4
 #endif
-constexpr int kLaneU = DLS_LANE_U;  // clients per batch on lane-channel tiles
+constexpr int kLaneUS = DLS_LANE_US;  // clients per batch on lane-channel tiles (staged path)
 #ifndef DLS_LANE_SCHED
 #define DLS_LANE_SCHED 2
 #endif
@@ -87,6 +87,31 @@ __device__ __forceinline__ void chunk_pipeline(int n, Load load, Consume consume
         j = nb * U;
     }
     for (; j < n; ++j) single(j);
+}
+
+// The same walk with the drain written so that no batch's code appears in both
+// arms of a branch (the compiler hoists such a common prefix, and with it every
+// conversion of the batch, above the first scheduling barrier).
+template <int U, class Batch, class Load, class Consume, class Single>
+__device__ __forceinline__ void chunk_pipeline_1tail(int n, Load load, Consume consume,
+                                                     Single single) {
+    const int nb = n / U;
+    if (nb > 0) {
+        Batch A, B;
+        load(0, A);
+        int b = 0;
+        for (; b + 2 < nb; b += 2) {
+            load((b + 1) * U, B);
+            consume(A);
+            load((b + 2) * U, A);
+            consume(B);
+        }
+        const bool two = b + 1 < nb;
+        if (two) load((b + 1) * U, B);
+        consume(A);
+        if (two) consume(B);
+    }
+    for (int j = nb * U; j < n; ++j) single(j);
 }
 
 struct ChunkRows {
@@ -157,6 +182,62 @@ __device__ __forceinline__ void accum16_one(float (&acc)[16], u32x4 qv, float s,
         // keep the scheduler from widening the chain over all 16 elements of
         // every in-flight client (that costs ~60 VGPRs and waves per SIMD)
         if (SCHED > 0 && (j / 2) % SCHED == SCHED - 1) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// The common path of the lane tiles: sz = (s, -fl(z*s)) from the wave's LDS
+// table.  Per step two element pairs, (j, j+1) and (j+8, j+9), as independent
+// chains interleaved by hand: a packed op that reads the result of the packed op
+// issued just before it costs an s_nop (4 cycles, as much as the op itself), and
+// the compiler's schedule serialised the two chains (a third of the issue slots
+// were s_nops).  The two-constant division (TWO) runs in the asm block;
+// Markstein's (its rare fallback divisors) in plain code.  Each step ends in a
+// scheduling barrier so that no later conversion is hoisted above it (hoisting
+// all of a batch's conversions cost ~40 VGPRs).
+template <bool SEXT, bool TWO>
+__device__ __forceinline__ void accum16_pk(float (&acc)[16], u32x4 qv, f32x2 sz, float wk,
+                                           const FastDiv &d) {
+    const f32x2 w2 = f32x2{wk, wk};
+    const f32x2 b2 = f32x2{d.b, d.b}, y2 = f32x2{d.y, d.y}, yl2 = f32x2{d.yl, d.yl};
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const int k = j & 3;
+        const f32x2 xa = f32x2{byte_val<SEXT>(qv[j >> 2], k), byte_val<SEXT>(qv[j >> 2], k + 1)};
+        const f32x2 xb = f32x2{byte_val<SEXT>(qv[(j >> 2) + 2], k),
+                               byte_val<SEXT>(qv[(j >> 2) + 2], k + 1)};
+        f32x2 ra = f32x2{acc[j], acc[j + 1]}, rb = f32x2{acc[j + 8], acc[j + 9]};
+        if constexpr (TWO) {
+            f32x2 ta, tb, la, lb;
+            asm volatile(
+                "v_pk_fma_f32 %[ta], %[xa], %[sz], %[sz] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+                "v_pk_fma_f32 %[tb], %[xb], %[sz], %[sz] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+                "v_pk_mul_f32 %[ta], %[w], %[ta]\n\t"
+                "v_pk_mul_f32 %[tb], %[w], %[tb]\n\t"
+                "v_pk_mul_f32 %[la], %[yl], %[ta]\n\t"
+                "v_pk_mul_f32 %[lb], %[yl], %[tb]\n\t"
+                "v_pk_fma_f32 %[ta], %[ta], %[y], %[la]\n\t"
+                "v_pk_fma_f32 %[tb], %[tb], %[y], %[lb]\n\t"
+                "v_pk_add_f32 %[ra], %[ra], %[ta]\n\t"
+                "v_pk_add_f32 %[rb], %[rb], %[tb]"
+                : [ra] "+v"(ra), [rb] "+v"(rb), [ta] "=&v"(ta), [tb] "=&v"(tb), [la] "=&v"(la),
+                  [lb] "=&v"(lb)
+                : [xa] "v"(xa), [xb] "v"(xb), [sz] "v"(sz), [w] "s"(w2), [yl] "s"(yl2),
+                  [y] "s"(y2));
+        } else {
+            auto term = [&](f32x2 x) {
+                const f32x2 t = pk_fma(x, sz.xx, sz.yy) * w2;
+                const f32x2 q0 = t * y2;
+                return pk_fma(pk_fma(-q0, b2, t), y2, q0);
+            };
+            ra = ra + term(xa);
+            rb = rb + term(xb);
+            asm volatile("" : "+v"(ra), "+v"(rb));
+        }
+        acc[j] = ra.x;
+        acc[j + 1] = ra.y;
+        acc[j + 8] = rb.x;
+        acc[j + 9] = rb.y;
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -523,19 +604,37 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
 // Multi-channel tiles of up to 4 KiB (every int tensor whose channel rows are a
 // multiple of 16 elements, so no lane's 16-element chunk straddles two channels:
 // the 3x3 convs of ResNet-18 / VGG-16, 576-4608-element rows).  Slice g of the
-// tile is lanes' chunks 1024 g + 16 lane, each lane in its own channel, so every
-// client step loads the lane's (scale, zero point) per slice beside its payload
-// (8 B, a few distinct lines per wave); the wave walks the clients once for all
-// its slices, double-buffered like the one-channel tiles.
+// tile is lanes' chunks 1024 g + 16 lane, each lane in its own channel; the wave
+// walks the clients once for all its slices, double-buffered like the
+// one-channel tiles.
+//
+// Per-lane (scale, zero point): a tile spans `span` consecutive channels.  When
+// span <= kSpanMax the wave stages them once per 64-client chunk: lane j loads
+// client j's pairs of those channels (a chunk ahead, coalesced: the table is
+// channel-major), checks the fast-path conditions for all of them at once (one
+// ballot per chunk) and writes (s, s, -fl(z*s), -fl(z*s)) to the wave's LDS
+// table; every client step then reads the lane's constants with one broadcast
+// ds_read_b128 per slice instead of a per-lane 8-byte global gather (which
+// doubled the vector-memory instructions and the texture data path's load)
+// and the per-client check.  Chunks that fail the check, and tiles spanning
+// more channels, take the per-client path: (scale, zero point) gathered per
+// lane with each client's payload and the check per client.
+constexpr int kSpanMax = 4;
+
 template <bool SIGNED, int G, bool TWO>
 __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                           int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                           const int32_t *__restrict__ rows,
                                           const float *__restrict__ w, int K, const FastDiv &d,
                                           float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) f32x2 stab[kBlock / 64][kSpanMax][64];
+    f32x2(*tab)[64] = stab[threadIdx.x >> 6];
     float acc[G][16];
     uint32_t qoff[G];
     int64_t coff[G];  // the lane's channel in slice g, in (scale, zp) pairs
+    uint32_t toff[G];  // its row of the LDS table, in pairs
+    const int span = (wt.t.row_pos + wt.t.len - 1) / wt.t.row_len + 1;  // wave-uniform
+    const bool staged = span <= kSpanMax;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
 #pragma unroll
@@ -543,23 +642,91 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         const int e0 = 1024 * g + 16 * __lane_id();
         const int ec = e0 < wt.lenpad ? e0 : wt.lenpad - 16;  // idle lanes: a valid duplicate
         qoff[g] = (uint32_t)(wt.t.src + ec);
-        const int c = min(wt.t.chan0 + (wt.t.row_pos + ec) / wt.t.row_len, wt.t.chan_end - 1);
+        const int crel = min((wt.t.row_pos + ec) / wt.t.row_len, span - 1);
+        const int c = min(wt.t.chan0 + crel, wt.t.chan_end - 1);
         coff[g] = (int64_t)c * L.chan;
+        toff[g] = (uint32_t)min(crel, kSpanMax - 1) * 64;
     }
+    // channel c of the tile (clamped into the tensor), client row r
+    auto tab_load = [&](int r, f32x2 (&v)[kSpanMax]) {
+#pragma unroll
+        for (int c = 0; c < kSpanMax; ++c)
+            v[c] = sz[(int64_t)min(wt.t.chan0 + c, wt.t.chan_end - 1) * L.chan + (int64_t)r * L.row];
+    };
     struct One {
         u32x4 qv[G];
         f32x2 s[G];
         float wk;
     };
-    struct Batch {
-        One c[kLaneU];
+    struct SOne {
+        u32x4 qv[G];
+        float wk;
+        int j;
+    };
+    struct SBatch {
+        SOne c[kLaneUS];
     };
     ChunkRows cr;
     cr.init(rows, w, K);
+    f32x2 nsz[kSpanMax];
+    if (staged) tab_load(cr.r0, nsz);
     for (int base = 0; base < K; base += 64) {
         const int tr = cr.r0;
         const float tw = cr.w0;
+        f32x2 tsz[kSpanMax];
+#pragma unroll
+        for (int c = 0; c < kSpanMax; ++c) tsz[c] = nsz[c];
+        if (staged) tab_load(cr.r1, nsz);  // next chunk (its rows landed a chunk ago)
         cr.advance(rows, w, K, base);
+        const int n = min(64, K - base);
+        bool allfast = false;
+        if (staged) {
+            // every (client, channel) of the chunk on the common path: exact fl(z*s)
+            // and the fast division range (always, for symmetric int8)
+            int ok = d.fast;
+#pragma unroll
+            for (int c = 0; c < kSpanMax; ++c) {
+                const float s = tsz[c].x, zs = tsz[c].y * s;
+                ok &= (int)(c >= span) |
+                      ((int)(__builtin_fmaf(tsz[c].y, s, -zs) == 0.f) & (int)scale_fast(s * tw));
+                tab[c][__lane_id()] = f32x2{s, -zs};
+            }
+            allfast = __ballot(!ok && __lane_id() < n) == 0;
+        }
+        if (allfast) {
+            auto sfetch = [&](int j, SOne &b) {
+                const int64_t r = readlane_i(tr, j);
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+                b.wk = readlane_f(tw, j);
+                b.j = j;
+            };
+            auto sstep = [&](const SOne &b) {
+                // the lane's (s, -zs): a broadcast LDS read (<= kSpanMax addresses per wave)
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    accum16_pk<SIGNED, TWO>(acc[g], b.qv[g], tab[0][toff[g] + b.j], b.wk, d);
+            };
+            chunk_pipeline_1tail<kLaneUS, SBatch>(
+                n,
+                [&](int j0, SBatch &b) {
+#pragma unroll
+                    for (int u = 0; u < kLaneUS; ++u) sfetch(j0 + u, b.c[u]);
+                },
+                [&](const SBatch &b) {
+#pragma unroll
+                    for (int u = 0; u < kLaneUS; ++u) sstep(b.c[u]);
+                },
+                [&](int j) {
+                    SOne b;
+                    sfetch(j, b);
+                    sstep(b);
+                });
+            continue;
+        }
         auto fetch = [&](int j, One &b) {
             const int64_t r = readlane_i(tr, j);
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -593,16 +760,10 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
                                                       b.wk, d);
             }
         };
-        chunk_pipeline<kLaneU, Batch>(
-            min(64, K - base),
-            [&](int j0, Batch &b) {
-#pragma unroll
-                for (int u = 0; u < kLaneU; ++u) fetch(j0 + u, b.c[u]);
-            },
-            [&](const Batch &b) {
-#pragma unroll
-                for (int u = 0; u < kLaneU; ++u) step(b.c[u]);
-            },
+        // one client per batch, double-buffered: these registers stay within the
+        // staged path's
+        chunk_pipeline<1, One>(
+            n, [&](int j0, One &b) { fetch(j0, b); }, [&](const One &b) { step(b); },
             [&](int j) {
                 One b;
                 fetch(j, b);
