@@ -20,7 +20,7 @@ constexpr int kQuantU = 2;      // clients per batch (1 KiB tiles); two batches 
 constexpr int kQuantUG = 1;     // clients per batch on multi-KiB tiles
 constexpr int kQuantSched = 2;  // element pairs between scheduling barriers
 #ifndef DLS_LANE_US
-#define DLS_LANE_US 4
+#define DLS_LANE_US 2
 #endif
 constexpr int kLaneUS = DLS_LANE_US;  // clients per batch on lane-channel tiles (staged path)
 #ifndef DLS_LANE_SCHED

@@ -339,11 +339,12 @@ class _ShardedShapleyMixin(_ShardedMixin):
         local = list(self.parameters.keys())
         kmax = max(1, -(-self.worker_number // self.world_size))
         buf = torch.zeros((kmax, P), dtype=torch.float32, device=self.device)
-        meta = torch.full((kmax, 2), -1, dtype=torch.int64, device=self.device)
         for j, wid in enumerate(local):
             buf[j].copy_(store.row(self.parameters.row_of(wid)))
-            meta[j, 0] = wid
-            meta[j, 1] = self.parameters.n_of(wid)
+        # built on the host, one host -> device copy
+        meta = [[int(wid), self.parameters.n_of(wid)] for wid in local]
+        meta += [[-1, 0]] * (kmax - len(meta))
+        meta = torch.tensor(meta, dtype=torch.int64).to(self.device)
         bufs = [torch.empty_like(buf) for _ in range(self.world_size)]
         metas = [torch.empty_like(meta) for _ in range(self.world_size)]
         dist.all_gather(bufs, buf, group=self.group)
