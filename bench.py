@@ -54,12 +54,28 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def timed_launches(fn, steps, warmup, sync_all=None):
-    """Run fn() warmup+steps times; HIP events around every timed launch on the
+# Single-GPU components warm up for at least this long before their timed
+# launches: a kernel's time ramps over its first ~20-40 back-to-back launches
+# (tools/launch_series.py: the sign vote 0.453 ms median over launches 0-19,
+# 0.417-0.419 from launch 40 on), so a 5-launch warmup timed the ramp.  The
+# headline keeps exactly the CLI's W warmup steps (the driver's contract), and so
+# do the sharded components (their launches hold collectives: every rank must run
+# the same count).
+COMPONENT_WARM_S = 0.1
+
+
+def timed_launches(fn, steps, warmup, sync_all=None, warm_s=0.0):
+    """Run fn() warmup+steps times (plus further untimed launches until warm_s
+    seconds of warmup have passed); HIP events around every timed launch on the
     current stream.  Returns (wall_s, [kernel_ms...])."""
+    t0 = time.perf_counter()
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
+    while time.perf_counter() - t0 < warm_s:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
     if sync_all:
         sync_all()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -241,7 +257,7 @@ def bench_fedavg_k1000(args, dev):
         if b is not None:
             b.record()
 
-    wall, kms = timed_launches(step, max(3, args.steps // 4), 2)
+    wall, kms = timed_launches(step, max(3, args.steps // 4), 2, warm_s=COMPONENT_WARM_S)
     ms = wall / max(3, args.steps // 4) * 1e3
     del U
     return {"config": "FedAvg of 1000 ResNet-18 fp32 updates (44.7 GB), bit-exact reference order",
@@ -267,7 +283,7 @@ def bench_sign(args, dev):
         if b is not None:
             b.record()
 
-    wall, kms = timed_launches(step, args.steps, args.warmup)
+    wall, kms = timed_launches(step, args.steps, args.warmup, warm_s=COMPONENT_WARM_S)
     ms = wall / args.steps * 1e3
     wire = W * 8
     bytes_per_launch = K * wire + P * 4 + wire  # client planes in, fp32 signs + packed vote out
@@ -282,7 +298,7 @@ def bench_sign(args, dev):
         if b is not None:
             b.record()
 
-    _, pkms = timed_launches(pstep, args.steps, args.warmup)
+    _, pkms = timed_launches(pstep, args.steps, args.warmup, warm_s=COMPONENT_WARM_S)
     del planes, X
     return {
         "config": "signSGD majority vote, 1000 clients x ResNet-18 (2-bit planes in; fp32 "
@@ -409,7 +425,7 @@ def bench_quant(args, dev, K=100, shapes=None, model="VGG-16", key="fed_quant"):
             b.record()
 
     steps = args.steps if K <= 100 else max(3, args.steps // 4)
-    wall, kms = timed_launches(step, steps, min(args.warmup, 3))
+    wall, kms = timed_launches(step, steps, min(args.warmup, 3), warm_s=COMPONENT_WARM_S)
     ms = wall / steps * 1e3
     bytes_per_launch = K * client_bytes + 4 * store.layout.numel
     # VALU roof at the reference's minimum op count: per int8 element and client
@@ -531,7 +547,7 @@ def bench_shapley_exact(args, dev):
         if b is not None:
             b.record()
 
-    wall, kms = timed_launches(step, args.steps, args.warmup)
+    wall, kms = timed_launches(step, args.steps, args.warmup, warm_s=COMPONENT_WARM_S)
     ms = wall / args.steps * 1e3
     pairs = sum(len(c) for c in subs)
     # minimum VALU lane-ops: per parameter, per (client, coalition) membership the
@@ -559,7 +575,7 @@ def bench_shapley_exact(args, dev):
         if b is not None:
             b.record()
 
-    _, kms_pc = timed_launches(step_pc, max(3, args.steps // 4), 1)
+    _, kms_pc = timed_launches(step_pc, max(3, args.steps // 4), 1, warm_s=COMPONENT_WARM_S)
     del U, out
     return {
         "config": f"Shapley subset models, default bit-exact path: {S} coalitions (members p=1/2, "
@@ -595,7 +611,7 @@ def bench_shapley_gemm(args, dev):
         if b is not None:
             b.record()
 
-    wall, kms = timed_launches(step, args.steps, args.warmup)
+    wall, kms = timed_launches(step, args.steps, args.warmup, warm_s=COMPONENT_WARM_S)
     ms = wall / args.steps * 1e3
     flops = 2.0 * S * K * layout.numel
     bytes_per_launch = (K + S) * P * 4
@@ -694,7 +710,7 @@ def bench_bn_act(args, dev):
         if eb is not None:
             eb.record()
 
-    _, kms = timed_launches(step, max(10, args.steps), 3)
+    _, kms = timed_launches(step, max(10, args.steps), 3, warm_s=COMPONENT_WARM_S)
     nbytes = x.numel() * 12
     del x, r, y
     return {"config": "eval BN + residual + ReLU, [1000, 64, 32, 32] fp32 channels_last",
