@@ -72,6 +72,8 @@ SIGNATURES = {
                             _i32),
     "dls_bn_fold_f32": ([_p, _p, _p, _p, _f32, _i32, _p, _p, _p], _i32),
     "dls_bn_act_nhwc_f32": ([_p, _i64, _i32, _p, _p, _p, _i32, _p, _p], _i32),
+    "dls_bn_fold_exact_f32": ([_p, _p, _p, _p, _f32, _i32, _p, _p], _i32),
+    "dls_bn_act_exact_nhwc_f32": ([_p, _i64, _i32, _p, _p, _i32, _p, _p], _i32),
 }
 
 _lib = None
@@ -299,4 +301,29 @@ def bn_act_nhwc(x, alpha, beta, residual=None, relu=True, out=None, inplace=Fals
     _check(lib().dls_bn_act_nhwc_f32(_ptr(x), N * H * W, C, _ptr(alpha), _ptr(beta),
                                      _ptr(residual), int(bool(relu)), _ptr(out),
                                      _stream(stream, x)), "dls_bn_act_nhwc_f32")
+    return out
+
+
+def bn_fold_exact(bn, consts, stream=None):
+    """The GPU library's eval batch-norm constants of a BatchNorm module into
+    consts [4*C] = [mean | iv | w | b] (dls_bn_fold_exact_f32)."""
+    _check(lib().dls_bn_fold_exact_f32(_ptr(bn.weight), _ptr(bn.bias), _ptr(bn.running_mean),
+                                       _ptr(bn.running_var), float(bn.eps), bn.num_features,
+                                       _ptr(consts), _stream(stream, consts)),
+           "dls_bn_fold_exact_f32")
+
+
+def bn_act_exact_nhwc(x, consts, residual=None, relu=True, out=None, inplace=False, stream=None):
+    """y = act(fma(w, (x - mean) * iv, b) [+ residual]) over a channels_last
+    [N, C, H, W] fp32 activation in one pass (dls_bn_act_exact_nhwc_f32)."""
+    N, C, H, W = x.shape
+    cl = torch.channels_last
+    if not x.is_contiguous(memory_format=cl) or (
+            residual is not None and not residual.is_contiguous(memory_format=cl)):
+        raise RuntimeError("bn_act_exact_nhwc: activations must be channels_last contiguous")
+    if out is None:
+        out = x if inplace else torch.empty_like(x, memory_format=cl)
+    _check(lib().dls_bn_act_exact_nhwc_f32(_ptr(x), N * H * W, C, _ptr(consts), _ptr(residual),
+                                           int(bool(relu)), _ptr(out),
+                                           _stream(stream, x)), "dls_bn_act_exact_nhwc_f32")
     return out

@@ -85,10 +85,134 @@ __global__ __launch_bounds__(kBnBlock) void k_bn_act(const f32x4 *x, int64_t n4,
     }
 }
 
+// The same pass with the per-channel arithmetic of the GPU library the reference
+// model's own eval forward runs on this stack (torch's eval BatchNorm2d goes to
+// MIOpen's MIOpenBatchNormFwdInferSpatialEst: inhat = (x - mean) * invVariance,
+// out = mad(scale, inhat, bias), invVariance = rsqrt(|var + eps|) per channel):
+//     y = act(fma(w_c, fl(fl(x - mean_c) * iv_c), b_c) [+ r])
+// consts = [mean | iv | w | b], C floats each (k_bn_fold_exact), iv by v_rsq_f32
+// and the multiply-add fused, as that kernel compiles here: bit-identical to the
+// module's forward (tests/test_gpu_infer.py; the correctly rounded 1/sqrt, or an
+// unfused multiply-add, differ on 10-60 % of the elements), so the fused ResNet
+// forward is the same function as model(x), one HBM pass per batch norm (+ the
+// residual add and ReLU after it) instead of three.
+__global__ __launch_bounds__(kBnBlock) void k_bn_fold_exact(const float *__restrict__ w,
+                                                            const float *__restrict__ b,
+                                                            const float *__restrict__ mean,
+                                                            const float *__restrict__ var,
+                                                            float eps, int C,
+                                                            float *__restrict__ consts) {
+    const int c = blockIdx.x * kBnBlock + threadIdx.x;
+    if (c >= C) return;
+    consts[c] = mean[c];
+    consts[C + c] = __builtin_amdgcn_rsqf(fabsf(var[c] + eps));  // v_rsq_f32
+    consts[2 * C + c] = w ? w[c] : 1.f;
+    consts[3 * C + c] = b ? b[c] : 0.f;
+}
+
+template <bool FIXED, bool RES, bool RELU>
+__global__ __launch_bounds__(kBnBlock) void k_bn_act_exact(const f32x4 *x, int64_t n4, int C4,
+                                                           const f32x4 *__restrict__ consts,
+                                                           const f32x4 *r, f32x4 *y) {
+    const int64_t stride = (int64_t)gridDim.x * kBnBlock;
+    int64_t i = (int64_t)blockIdx.x * kBnBlock + threadIdx.x;
+    f32x4 m = {}, iv = {}, wv = {}, bv = {};
+    auto consts_of = [&](int cg) {
+        m = consts[cg];
+        iv = consts[C4 + cg];
+        wv = consts[2 * C4 + cg];
+        bv = consts[3 * C4 + cg];
+    };
+    if (FIXED) consts_of((int)(i % C4));
+    auto one = [&](f32x4 v, f32x4 rv, int64_t k) {
+        if (!FIXED) consts_of((int)(k % C4));
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float h = (v[e] - m[e]) * iv[e];
+            float t = __builtin_fmaf(wv[e], h, bv[e]);
+            if (RES) t = t + rv[e];
+            if (RELU) t = t > 0.f ? t : (t == t ? 0.f : t);  // relu keeps NaN, as torch
+            o[e] = t;
+        }
+        return o;
+    };
+    for (; i + (kBnUnroll - 1) * stride < n4; i += kBnUnroll * stride) {
+        f32x4 v[kBnUnroll], rv[kBnUnroll];
+#pragma unroll
+        for (int u = 0; u < kBnUnroll; ++u) {
+            v[u] = __builtin_nontemporal_load(x + i + u * stride);
+            if (RES) rv[u] = __builtin_nontemporal_load(r + i + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < kBnUnroll; ++u)
+            y[i + u * stride] = one(v[u], RES ? rv[u] : f32x4{}, i + u * stride);
+    }
+    for (; i < n4; i += stride) {
+        const f32x4 v = x[i];
+        y[i] = one(v, RES ? r[i] : f32x4{}, i);
+    }
+}
+
 }  // namespace
 }  // namespace dls
 
 using namespace dls;
+
+extern "C" int dls_bn_fold_exact_f32(const float *weight, const float *bias, const float *mean,
+                                     const float *var, float eps, int32_t C, float *consts,
+                                     dls_stream_t stream) {
+    DLS_REQUIRE(mean && var && consts, DLS_EINVAL, "dls_bn_fold_exact_f32: null pointer");
+    DLS_REQUIRE(C > 0, DLS_EINVAL, "dls_bn_fold_exact_f32: C=%d", C);
+    hipLaunchKernelGGL(k_bn_fold_exact, dim3((unsigned)((C + kBnBlock - 1) / kBnBlock)),
+                       dim3(kBnBlock), 0, as_stream(stream), weight, bias, mean, var, eps, (int)C,
+                       consts);
+    return check_launch("dls_bn_fold_exact_f32");
+}
+
+extern "C" int dls_bn_act_exact_nhwc_f32(const float *x, int64_t rows, int32_t C,
+                                         const float *consts, const float *residual, int32_t relu,
+                                         float *y, dls_stream_t stream) {
+    DLS_REQUIRE(x && consts && y, DLS_EINVAL, "dls_bn_act_exact_nhwc_f32: null pointer");
+    DLS_REQUIRE(rows > 0 && C > 0 && C % 4 == 0, DLS_EINVAL,
+                "dls_bn_act_exact_nhwc_f32: rows=%lld C=%d (C a multiple of 4)", (long long)rows, C);
+    DLS_REQUIRE(aligned16(x) && aligned16(y) && aligned16(consts) &&
+                    (!residual || aligned16(residual)),
+                DLS_ELAYOUT, "dls_bn_act_exact_nhwc_f32: 16-byte alignment");
+    const int64_t n4 = rows * (C / 4);
+    const int C4 = C / 4;
+    int64_t blocks = (n4 + (int64_t)kBnBlock * kBnUnroll - 1) / ((int64_t)kBnBlock * kBnUnroll);
+    const int64_t cap = (int64_t)resident_blocks(reinterpret_cast<const void *>(
+                                                     k_bn_act_exact<true, false, true>),
+                                                 kBnBlock, 0) * 4;
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    const bool fixed = ((int64_t)kBnBlock * blocks) % C4 == 0;
+    const f32x4 *xv = reinterpret_cast<const f32x4 *>(x);
+    const f32x4 *cv = reinterpret_cast<const f32x4 *>(consts);
+    const f32x4 *rv = reinterpret_cast<const f32x4 *>(residual);
+    f32x4 *yv = reinterpret_cast<f32x4 *>(y);
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)blocks), block(kBnBlock);
+    const bool res = residual != nullptr;
+#define DLS_BNX(F_, R_, A_) \
+    hipLaunchKernelGGL((k_bn_act_exact<F_, R_, A_>), grid, block, 0, st, xv, n4, C4, cv, rv, yv)
+    if (fixed) {
+        if (res) {
+            if (relu) DLS_BNX(true, true, true); else DLS_BNX(true, true, false);
+        } else {
+            if (relu) DLS_BNX(true, false, true); else DLS_BNX(true, false, false);
+        }
+    } else {
+        if (res) {
+            if (relu) DLS_BNX(false, true, true); else DLS_BNX(false, true, false);
+        } else {
+            if (relu) DLS_BNX(false, false, true); else DLS_BNX(false, false, false);
+        }
+    }
+#undef DLS_BNX
+    return check_launch("dls_bn_act_exact_nhwc_f32");
+}
 
 extern "C" int dls_bn_fold_f32(const float *weight, const float *bias, const float *mean,
                                const float *var, float eps, int32_t C, float *alpha, float *beta,

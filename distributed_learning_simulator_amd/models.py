@@ -44,17 +44,19 @@ class _Block(nn.Module):
 
     def forward_fused(self, x, fold):
         """Eval-mode forward on channels_last activations: each batch norm (with the
-        ReLU / residual add after it) is one dls_bn_act_nhwc_f32 pass, in place on
-        the convolution's output; same op order as forward()."""
+        ReLU / residual add after it) is one dls_bn_act_exact_nhwc_f32 pass, in
+        place on the convolution's output; the same ops and roundings as forward()
+        on the GPU, so the same bits."""
         from . import _native
-        out = _native.bn_act_nhwc(self.conv1(x), *fold[id(self.bn1)], relu=True, inplace=True)
+        out = _native.bn_act_exact_nhwc(self.conv1(x), fold[id(self.bn1)], relu=True, inplace=True)
         out = self.conv2(out)
         if len(self.shortcut):
-            sc = _native.bn_act_nhwc(self.shortcut[0](x), *fold[id(self.shortcut[1])], relu=False,
-                                     inplace=True)
+            sc = _native.bn_act_exact_nhwc(self.shortcut[0](x), fold[id(self.shortcut[1])],
+                                           relu=False, inplace=True)
         else:
             sc = x
-        return _native.bn_act_nhwc(out, *fold[id(self.bn2)], residual=sc, relu=True, inplace=True)
+        return _native.bn_act_exact_nhwc(out, fold[id(self.bn2)], residual=sc, relu=True,
+                                         inplace=True)
 
 
 class ResNet18(nn.Module):
@@ -83,24 +85,26 @@ class ResNet18(nn.Module):
 
     @torch.no_grad()
     def fold_bn(self):
-        """{id(bn): (alpha, beta)} of every batch norm for forward_fused (eval mode,
-        running statistics; recomputed per evaluation since the weights change)."""
+        """{id(bn): consts [4*C] = [mean | iv | w | b]} of every batch norm for
+        forward_fused (eval mode, running statistics; recomputed per evaluation
+        since the weights change; dls_bn_fold_exact_f32)."""
         from . import _native
         fold = {}
         for m in self.modules():
             if isinstance(m, nn.BatchNorm2d):
-                a = torch.empty(m.num_features, device=m.running_mean.device)
-                b = torch.empty_like(a)
-                _native.bn_fold(m, a, b)
-                fold[id(m)] = (a, b)
+                c = torch.empty(4 * m.num_features, device=m.running_mean.device)
+                _native.bn_fold_exact(m, c)
+                fold[id(m)] = c
         return fold
 
     def forward_fused(self, x, fold):
         """forward() for utility evaluation on the GPU: channels_last activations,
         MIOpen convolutions, every batch norm + ReLU (+ residual add) fused into one
-        hand-written pass (dls_bn_act_nhwc_f32)."""
+        hand-written pass (dls_bn_act_exact_nhwc_f32) with the batch-norm library's
+        own arithmetic: the logits are bit-identical to forward()'s
+        (tests/test_gpu_infer.py)."""
         from . import _native
-        out = _native.bn_act_nhwc(self.conv1(x), *fold[id(self.bn1)], relu=True, inplace=True)
+        out = _native.bn_act_exact_nhwc(self.conv1(x), fold[id(self.bn1)], relu=True, inplace=True)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 out = blk.forward_fused(out, fold)

@@ -46,15 +46,15 @@ class Inferencer:
     """The tester (ref servers/fed_server.py:26-32): top-1 accuracy / mean loss of
     ``model`` over ``dataset``.
 
-    ``fused_eval=True`` (opt-in) runs models that have a ``forward_fused`` eval
-    path (models.ResNet18) with every batch norm + ReLU (+ residual add) as one
-    hand-written NHWC pass (dls_bn_act_nhwc_f32): ~1.8x faster utility
-    evaluations, logits within 1e-4 (normwise) of the module forward, so an
-    accuracy utility may differ by a near-tied prediction (tests/test_gpu_infer.py
-    allows 2/600).  The default is the module's own forward, so Shapley utilities
-    are those of the plain PyTorch-ROCm model."""
+    Models that have a ``forward_fused`` eval path (models.ResNet18) run it on the
+    GPU (``fused_eval``, default on): every batch norm + ReLU (+ residual add) as
+    one hand-written NHWC pass (dls_bn_act_exact_nhwc_f32) with the batch-norm
+    library's own arithmetic, ~1.8x faster utility evaluations whose logits are
+    bit-identical to the module's forward (tests/test_gpu_infer.py), so Shapley
+    utilities are those of the plain PyTorch-ROCm model either way.
+    ``fused_eval=False`` runs the module's forward."""
 
-    def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=False):
+    def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True):
         self.model = model
         self.fused_eval = fused_eval
         self.dataset = dataset
@@ -75,8 +75,8 @@ class Inferencer:
             # NHWC convolutions: measured 8-18 % faster than NCHW for this model family
             # on MI355X (tools/eval_probe.py); results are the same up to fp32 reassociation
             self.model.to(memory_format=torch.channels_last)
-        # fused_eval and a model with a fused eval forward (models.ResNet18): every batch
-        # norm + ReLU (+ residual add) is one hand-written NHWC pass instead of three kernels
+        # a model with a fused eval forward (models.ResNet18): every batch norm + ReLU
+        # (+ residual add) is one hand-written NHWC pass instead of three kernels
         fused = (getattr(self.model, "forward_fused", None)
                  if self.fused_eval and X.dim() == 4 and torch.device(self.device).type == "cuda"
                  else None)

@@ -242,6 +242,17 @@ int dls_bn_fold_f32(const float *weight, const float *bias, const float *mean, c
 int dls_bn_act_nhwc_f32(const float *x, int64_t rows, int32_t C, const float *alpha,
                         const float *beta, const float *residual, int32_t relu, float *y,
                         dls_stream_t stream);
+/* The same pass with the GPU library's eval batch-norm arithmetic (the reference
+ * model's own eval forward on this stack runs MIOpen's
+ * MIOpenBatchNormFwdInferSpatialEst): y = fma(w_c, fl(fl(x - mean_c) * iv_c), b_c),
+ * iv_c = v_rsq_f32(|var_c + eps|), then + residual and ReLU as above: bit-identical
+ * to torch's eval BatchNorm2d here.  dls_bn_fold_exact_f32 writes
+ * consts = [mean | iv | w | b] (4*C floats, 16-byte aligned). */
+int dls_bn_fold_exact_f32(const float *weight, const float *bias, const float *mean,
+                          const float *var, float eps, int32_t C, float *consts,
+                          dls_stream_t stream);
+int dls_bn_act_exact_nhwc_f32(const float *x, int64_t rows, int32_t C, const float *consts,
+                              const float *residual, int32_t relu, float *y, dls_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -5,10 +5,13 @@ servers/fed_server.py:26-32) with its hand-written eval batch norm.
   torch (alpha = 1/sqrt(var+eps) * w, beta = b - mean * alpha, y = x*alpha + beta,
   + residual, ReLU): bit-exact, every flag combination, ragged sizes, C not a
   divisor of the grid (the per-iteration channel path), in place.
-* ResNet-18 forward_fused vs torch's own eval forward (MIOpen batch norm):
-  logits within 1e-4 (relative, normwise per image) and identical predictions
-  on all but near-tied images; the Inferencer's accuracy equal.  Utility parity
-  with the reference's tester is unpinned (its library is absent).
+* dls_bn_fold_exact_f32 / dls_bn_act_exact_nhwc_f32 against torch's own eval
+  BatchNorm2d on the GPU (MIOpen's inference kernel), + residual, ReLU: bit-exact.
+* ResNet-18 forward_fused (the exact pass) vs torch's own eval forward: logits
+  bit-identical with MIOpen's deterministic convolutions (its default kernels for
+  the 512-channel layer vary run to run, the module's forward included); the
+  Inferencer's accuracy and loss equal on both paths.
+  Utility parity with the reference's tester is unpinned (its library is absent).
 """
 import numpy as np
 import pytest
@@ -71,7 +74,52 @@ def test_bn_act_rejects_nchw():
         _native.bn_act_nhwc(x, torch.ones(8, device=dev), torch.zeros(8, device=dev))
 
 
-def test_resnet18_fused_eval_matches_torch():
+@pytest.mark.parametrize("N,C,H,W", [(64, 64, 32, 32), (16, 128, 16, 16), (7, 512, 4, 4),
+                                     (3, 12, 5, 3), (2, 96, 3, 3)])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_bn_act_exact_matches_torch_eval(N, C, H, W, res, relu):
+    """The exact pass = torch's eval BatchNorm2d (+ residual add, ReLU) bit for bit,
+    channels_last fp32, NaN kept, in place."""
+    from distributed_learning_simulator_amd import _native
+    g = torch.Generator().manual_seed(N + C + H)
+    bn = _bn(C, g)
+    with torch.no_grad():
+        bn.running_var[0] = 1e-3  # small variances too
+    consts = torch.empty(4 * C, device=dev)
+    _native.bn_fold_exact(bn, consts)
+    cl = torch.channels_last
+    x = (torch.randn(N, C, H, W, generator=g) * 3).to(dev).contiguous(memory_format=cl)
+    x[0, 0, 0, 0] = float("nan")
+    r = torch.randn(N, C, H, W, generator=g).to(dev).contiguous(memory_format=cl) if res else None
+    with torch.no_grad():
+        ref = bn(x)
+        if res:
+            ref = ref + r
+        if relu:
+            ref = torch.relu(ref)
+    y = _native.bn_act_exact_nhwc(x, consts, residual=r, relu=relu)
+    assert y.is_contiguous(memory_format=cl)
+    assert torch.isnan(y[0, 0, 0, 0]) and torch.isnan(ref[0, 0, 0, 0])
+    m = ~torch.isnan(ref)
+    assert torch.equal(y[m].view(torch.int32), ref[m].view(torch.int32))
+    y2 = _native.bn_act_exact_nhwc(x.clone(memory_format=cl), consts, residual=r, relu=relu,
+                                   inplace=True)
+    assert torch.equal(y2[m].view(torch.int32), ref[m].view(torch.int32))
+
+
+@pytest.fixture
+def deterministic_convs():
+    """MIOpen's convolutions for ResNet-18's 512-channel layer pick a kernel whose
+    result varies between two runs of the same input (tools/diag_fused.py: the
+    module's own forward twice is not bit-identical); its deterministic mode makes
+    the module's forward a function, so the fused path can be compared bit for bit."""
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    yield
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+
+
+def test_resnet18_fused_eval_matches_torch(deterministic_convs):
     from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
     from distributed_learning_simulator_amd.trainer import Inferencer
     torch.manual_seed(0)
@@ -89,24 +137,20 @@ def test_resnet18_fused_eval_matches_torch():
     xb = X.to(dev).contiguous(memory_format=torch.channels_last)
     with torch.no_grad():
         ref = model(xb)
+        assert torch.equal(model(xb).view(torch.int32), ref.view(torch.int32))  # a function
         got = model.forward_fused(xb, model.fold_bn())
-    err = torch.linalg.norm(got - ref, dim=1) / torch.linalg.norm(ref, dim=1)
-    assert float(err.max()) < 1e-4, float(err.max())
-    top2 = torch.topk(ref, 2, dim=1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 1e-3 * top2[:, 0].abs().clamp_min(1e-6)
-    assert torch.equal(got.argmax(1)[clear], ref.argmax(1)[clear])
-    # fused_eval=True: the Inferencer takes the fused path on the GPU; accuracy as
-    # torch's forward up to near-tied predictions
-    inf = Inferencer(model, (X, y), batch_size=256, device=dev, fused_eval=True)
-    _, acc, _ = inf.inference()
-    ref_acc = float((ref.argmax(1).cpu() == y).float().mean())
-    assert abs(acc - ref_acc) <= 2 / 600
-    assert np.isfinite(float(inf.loss_metric.value))
-    # the default is the module's own forward: the accuracy of torch's eval forward
-    # over the same batches (MIOpen may pick other algorithms for other batch sizes)
-    plain = Inferencer(model, (X, y), batch_size=256, device=dev)
-    assert plain.fused_eval is False
-    _, acc0, _ = plain.inference()
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))  # the same bits
+    # the Inferencer takes the fused path on the GPU by default; fused_eval=False the
+    # module's forward: the same accuracy and loss, and those of torch's eval
+    # forward over the same batches (MIOpen may pick other algorithms for other
+    # batch sizes)
+    inf = Inferencer(model, (X, y), batch_size=256, device=dev)
+    assert inf.fused_eval is True
+    loss, acc, _ = inf.inference()
+    plain = Inferencer(model, (X, y), batch_size=256, device=dev, fused_eval=False)
+    loss0, acc0, _ = plain.inference()
+    assert acc == acc0 and float(loss) == float(loss0)
     with torch.no_grad():
         pred = torch.cat([model(xb[i:i + 256]).argmax(1) for i in range(0, xb.shape[0], 256)])
     assert acc0 == int((pred.cpu() == y).sum()) / y.numel()  # the Inferencer's int / n
+    assert np.isfinite(float(loss))

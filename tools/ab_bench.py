@@ -219,10 +219,10 @@ def setup(dev, want=()):
         bx = torch.randn(1000, 64, 32, 32, device=dev).contiguous(memory_format=torch.channels_last)
         br = torch.randn_like(bx)
         by = torch.empty_like(bx)
-        ba = torch.rand(64, device=dev) + 0.5
-        bb = torch.randn(64, device=dev)
-        W["bn_act"] = (lambda L: L.dls_bn_act_nhwc_f32(ptr(bx), 1000 * 32 * 32, 64, ptr(ba), ptr(bb),
-                                                        ptr(br), 1, ptr(by), stream()),
+        bc = torch.cat([torch.randn(64, device=dev), torch.rand(64, device=dev) + 0.5,
+                        torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev)])
+        W["bn_act"] = (lambda L: L.dls_bn_act_exact_nhwc_f32(ptr(bx), 1000 * 32 * 32, 64, ptr(bc),
+                                                              ptr(br), 1, ptr(by), stream()),
                        bx.numel() * 12)
     C = torch.rand((50, 50), generator=g, device=dev)
     C = C / C.sum(1, keepdim=True)
