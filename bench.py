@@ -487,7 +487,9 @@ def bench_config1(args, dev):
     FedServer.get_subset_model = timed_subset
     try:
         t0 = time.perf_counter()
-        server = simulator.run(cfg)
+        # one process, this rank's GPU: inside a multi-rank job the default would pick
+        # the sharded servers, whose collectives the other ranks never join
+        server = simulator.run(cfg, devices=[dev], sharded=False)
         wall = time.perf_counter() - t0
     finally:
         FedServer.get_subset_model = orig

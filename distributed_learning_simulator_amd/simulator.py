@@ -51,7 +51,11 @@ def get_cuda_devices():
     return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
 
 
-def run(config):
+def run(config, devices=None, sharded=None):
+    """simulator.py:33-72.  ``devices``: the GPUs the worker threads use (default all
+    visible); ``sharded``: get_server's (default: sharded servers when
+    torch.distributed is initialised with more than one rank) — a caller that runs
+    a one-process simulation inside a multi-rank job passes False."""
     log = logging.getLogger("distributed_learning_simulator_amd")
     log.setLevel(config.log_level)
     if config.log_dir:
@@ -65,10 +69,10 @@ def run(config):
     Xt, yt = synthetic_classification(config.test_size, shape, seed=config.seed + 1)
     torch.manual_seed(config.seed)
     model_cls = MODELS[config.model_name]
-    devices = get_cuda_devices()
+    devices = list(devices) if devices else get_cuda_devices()
     server_device = devices[0]
     tester = Inferencer(model_cls().to(server_device), (Xt, yt), device=server_device)
-    server = get_server(config.distributed_algorithm, tester=tester,
+    server = get_server(config.distributed_algorithm, sharded=sharded, tester=tester,
                         worker_number=config.worker_number, multi_process=False)
     # IID split (simulator.py:48-50)
     perm = torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(config.seed))
