@@ -3,10 +3,9 @@
 VGG-16) for store-layout knobs: LANE_TILE (lane-tile width) and, with
 DLS_HIP_LIB-style variant libraries, kernel builds.
 
-    python tools/quant_ab.py --lane 1024,2048,4096 [--lane-g 0,1,2,3] [--reps 5]
+    python tools/quant_ab.py --lane 1024,2048,4096 [--reps 5] [--check]
 
---lane-g: slices per wave of the lane kernel (DLS_LANE_G; 0 = the library's choice),
-timed interleaved for every lane-tile width; --check compares every output bit for bit.
+--check compares every width's output bit for bit with the first's.
 """
 import argparse
 import ctypes
@@ -47,7 +46,6 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--check", action="store_true")
-    ap.add_argument("--lane-g", default="0")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     shapes = resnet18_cifar() if args.model == "resnet18" else vgg16()
@@ -64,8 +62,7 @@ def main():
     rows = torch.arange(K, dtype=torch.int32, device=dev)
     w = torch.tensor(n, dtype=torch.float32, device=dev)
     total = float(sum(n))
-    gs = [int(x) for x in args.lane_g.split(",")]
-    cases = [(lt, g) for lt in lanes for g in gs]
+    cases = [(lt, 0) for lt in lanes]
     outs = {c: torch.empty(st.layout.P, device=dev) for c in cases}
     ql = st.qlayout
     Pq = sum(m for m, k in zip(st.layout.numels, ql.kinds) if k)
@@ -74,11 +71,7 @@ def main():
     res = {c: [] for c in cases}
     for r in range(args.reps):
         for c in cases:
-            lt, g = c
-            if g:
-                os.environ["DLS_LANE_G"] = str(g)
-            else:
-                os.environ.pop("DLS_LANE_G", None)
+            lt = c[0]
             tb, nt, nf = tables[lt]
             for _ in range(2):
                 _native.dequant_fedavg(tb, nt, nf, st.Q, st.F, st.sz, rows, w, total, outs[c])
@@ -89,10 +82,9 @@ def main():
             b.record()
             torch.cuda.synchronize()
             res[c].append(a.elapsed_time(b) / args.launches)
-    os.environ.pop("DLS_LANE_G", None)
     for c in cases:
         ms = sorted(res[c])[len(res[c]) // 2]
-        print(f"lane_tile {c[0]} G {c[1]}: nfast {tables[c[0]][2]} median {ms:.4f} ms  "
+        print(f"lane_tile {c[0]}: nfast {tables[c[0]][2]} median {ms:.4f} ms  "
               f"{nbytes / ms / 1e6:.1f} GB/s  frac {nbytes / ms / 1e6 / 8000:.4f}  all {['%.4f' % x for x in res[c]]}",
               flush=True)
     if args.check:
