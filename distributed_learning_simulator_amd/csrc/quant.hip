@@ -601,7 +601,7 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
     store_tile<G>(wt, acc, out);
 }
 
-// Multi-channel tiles of up to 4 KiB (every int tensor whose channel rows are a
+// Multi-channel tiles of 1 KiB (every int tensor whose channel rows are a
 // multiple of 16 elements, so no lane's 16-element chunk straddles two channels:
 // the 3x3 convs of ResNet-18 / VGG-16, 576-4608-element rows).  Slice g of the
 // tile is lanes' chunks 1024 g + 16 lane, each lane in its own channel; the wave
@@ -1239,6 +1239,12 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     }
     DLS_REQUIRE(ntiles > 0 && K > 0 && nf <= ntiles, DLS_EINVAL,
                 "dls_dequant_fedavg: ntiles=%d grouped tiles=%lld K=%d", ntiles, (long long)nf, K);
+    // multi-channel tiles are cut at 1 KiB (the wider lane kernels measured no
+    // faster and are not built): groups 4-6 stay in the numbering, empty
+    DLS_REQUIRE(nfast[4] == 0 && nfast[5] == 0 && nfast[6] == 0, DLS_EINVAL,
+                "dls_dequant_fedavg: multi-channel int tiles of 4/3/2 KiB (nfast[4..6] = %d, %d, "
+                "%d) are not supported; cut them into 1 KiB tiles (group 7)",
+                nfast[4], nfast[5], nfast[6]);
     DLS_REQUIRE(ldq % 16 == 0 && ldf % 4 == 0 && aligned16(out) && (!Q || aligned16(Q)) &&
                     (!F || aligned16(F)),
                 DLS_ELAYOUT, "dls_dequant_fedavg: ldq %% 16, ldf %% 4, 16-byte alignment");
@@ -1250,8 +1256,8 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
-    // Groups: 0-3 one-channel tiles of 4/3/2/1 KiB slices, 4-7 lane-channel tiles
-    // of 4/3/2/1 slices, 8 fp32 tiles, 9 small int tiles, then the general tiles.  The group with
+    // Groups: 0-3 one-channel tiles of 4/3/2/1 KiB slices, 7 lane-channel tiles
+    // of 1 KiB (4-6 empty), 8 fp32 tiles, 9 small int tiles, then the general tiles.  The group with
     // the most bytes runs on the caller's stream; every other non-empty group on a
     // side stream of its own, concurrently (their waves walk all K clients, so a
     // small group is a long latency chain, not a small amount of work), and the
@@ -1296,9 +1302,9 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
         {k_dequant_fast<3, false>, k_dequant_fast<3, true>},
         {k_dequant_fast<2, false>, k_dequant_fast<2, true>},
         {k_dequant_fast<1, false>, k_dequant_fast<1, true>},
-        {k_dequant_lanes<4, false>, k_dequant_lanes<4, true>},
-        {k_dequant_lanes<3, false>, k_dequant_lanes<3, true>},
-        {k_dequant_lanes<2, false>, k_dequant_lanes<2, true>},
+        {nullptr, nullptr},  // groups 4-6: rejected above
+        {nullptr, nullptr},
+        {nullptr, nullptr},
         {k_dequant_lanes<1, false>, k_dequant_lanes<1, true>}};
     // A wave walks all K clients, so waves are long and equal: a group is launched
     // in pieces of at most one generation of resident waves (a last generation of

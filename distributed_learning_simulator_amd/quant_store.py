@@ -28,7 +28,8 @@ from .layout import ALIGN, ParameterLayout, _round_up
 
 TILE = 1024  # one wavefront slice: 64 lanes x 16 elements
 FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
-LANE_TILE = 1024  # multi-channel tiles (channel rows a multiple of 16): slices per wavefront
+LANE_TILE = TILE  # multi-channel tiles (channel rows a multiple of 16): one slice per wavefront
+# (dls_dequant_fedavg rejects wider ones: their kernels measured no faster)
 F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
 FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
 QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
@@ -107,10 +108,10 @@ class QuantLayout:
           channel rows are long (>= 1024, multiple of 64) and fill 1 KiB slices
           well get channel-aligned tiles of up to FAST_TILE elements (a wave
           streams up to 4 KiB of every client row with one (scale, zp) per client);
-        * lane-channel tiles (groups 4-7): the other int tensors whose channel rows
-          are a multiple of 16 elements (no lane's 16-element chunk straddles two
-          channels: 3x3 convs, fc layers) are cut into LANE_TILE-element tiles from
-          their start, each lane loading its own channel's (scale, zp);
+        * lane-channel tiles (group 7; groups 4-6, wider ones, stay empty): the
+          other int tensors whose channel rows are a multiple of 16 elements (no
+          lane's 16-element chunk straddles two channels: 3x3 convs, fc layers) are
+          cut into 1 KiB tiles from their start, each lane in its own channel;
         * fp32 tiles (group 8, <= F32_TILE elements): the fp32 tensors;
         * small int tiles (group 9, <= F32_TILE elements): the other int tensors
           with rows of at least 4 elements (a lane's 4 span <= 2 channels), except
