@@ -149,7 +149,7 @@ def setup(dev, want=()):
                                                              100, tot, ptr(qo), stream()),
                               100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
     if any(w.startswith("quant_r18") for w in want):
-        # north-star: 1000 ResNet-18 int8 updates; quant_r18_l<N>: lane tiles of N KiB
+        # north-star: 1000 ResNet-18 int8 updates; quant_r18_l1_w<N>: FAST_WASTE = N
         from distributed_learning_simulator_amd import quant_store as qs
         from distributed_learning_simulator_amd.quant_store import QuantizedClientStore as QCS
         template = {}
@@ -173,7 +173,7 @@ def setup(dev, want=()):
                      4 * sum(m for m, k in zip(sr.layout.numels, qlr.kinds) if not k) + 8 * qlr.C) \
             + 4 * sr.layout.numel
         saved = qs.LANE_TILE
-        for lt, fwv in ((1, None), (2, None), (4, None), (1, 0), (1, 8), (1, 16)):
+        for lt, fwv in ((1, None), (1, 0), (1, 8), (1, 16)):  # lane tiles are 1 KiB
             qs.LANE_TILE = 1024 * lt
             fw, qs.FAST_WASTE = qs.FAST_WASTE, (qs.FAST_WASTE if fwv is None else fwv)
             tt, nft = qlr.tiles()
@@ -186,6 +186,22 @@ def setup(dev, want=()):
                     ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb, qo18)
         qs.LANE_TILE = saved
         W["quant_r18"] = W[f"quant_r18_l{saved // 1024}"]
+        if "quant_r18_slab" in want:
+            # slab-major emulation: every Q tile of <= 1 KiB gets its own slab of
+            # 1000 consecutive 1 KiB client pieces (ldq = 1 KiB, src = slab start),
+            # so a wave streams its slab sequentially
+            tt, nft = qlr.tiles()
+            ts = tt.copy()
+            isq = np.nonzero(ts["kind"] != 0)[0]
+            ts["src"][isq] = np.arange(len(isq), dtype=np.int64) * 1000 * 1024
+            Qs = torch.empty(len(isq) * 1000 * 1024, dtype=torch.uint8, device=dev)
+            Qs.random_(0, 256, generator=g)
+            tsd = torch.from_numpy(ts.view(np.uint8).copy()).to(dev)
+            W["quant_r18_slab"] = (
+                lambda L: L.dls_dequant_fedavg(
+                    ptr(tsd), len(ts), nfast_arg(L, nft), ptr(Qs), 1024, ptr(sr.F),
+                    sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
+                    ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb, qo18)
     # Shapley default path: 50 coalitions (members with p = 1/2) over 50 clients,
     # each client row read once per batch (dls_subset_fedavg_union_f32)
     from distributed_learning_simulator_amd.aggregation import union_batch

@@ -7,6 +7,12 @@ With CALLS (the number of C-ABI calls the traced command made), also prints the
 kernel time per call: one dls_fedavg_f32 call may launch its kernel as several
 one-generation pieces, so rocprof's per-launch average is a fraction of the
 per-call duration bench.py times with HIP events.
+
+    python tools/trace_summary.py --tail N gpurun_out/prof_<tag>/trace/kernel_trace_dls.csv
+
+per kernel, the average / min / max of its LAST N launches in the trace: the
+steady state of a bench component, whose first launches (the untimed warm-up,
+kernel times ramp over the first ~20-40 launches) the --stats average includes.
 """
 import csv
 import re
@@ -35,5 +41,23 @@ def main(path, calls=None):
               f"{tot / calls / 1e3:.2f} us of kernel time per call")
 
 
+def tail(path, n):
+    by = {}
+    for r in csv.DictReader(open(path)):
+        if "dls::" not in r["Kernel_Name"]:
+            continue
+        by.setdefault(short(r["Kernel_Name"]), []).append(
+            (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    print(f"# last {n} launches per kernel of {path}")
+    print(f"{'kernel':44s} {'launches':>8s} {'tail_avg_us':>11s} {'tail_min_us':>11s} {'tail_max_us':>11s}")
+    for k, v in sorted(by.items(), key=lambda kv: -sum(d for _, d in kv[1])):
+        d = [x for _, x in sorted(v)][-n:]
+        print(f"{k:44s} {len(v):8d} {sum(d) / len(d) / 1e3:11.2f} {min(d) / 1e3:11.2f} "
+              f"{max(d) / 1e3:11.2f}")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
+    if sys.argv[1] == "--tail":
+        tail(sys.argv[3], int(sys.argv[2]))
+    else:
+        main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
