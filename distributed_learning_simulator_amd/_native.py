@@ -66,6 +66,8 @@ SIGNATURES = {
     "dls_dequant_fedavg": ([_p, _i32, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _p, _i32, _f32,
                             _p, _p],
                            _i32),
+    "dls_dequant_fedavg_mode": ([_p, _i32, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _p, _i32,
+                                 _f32, _i32, _p, _p], _i32),
     "dls_segment_minmax_f32": ([_p, _p, _i32, _p, _p, _i64, _p], _i32),
     "dls_qparams_minmax": ([_p, _p, _i32, _i32, _i32, _i32, _p, _p, _p], _i32),
     "dls_quantize_affine": ([_p, _p, _i32, _p, _p, _i32, _i32, _p, _p, _i32, _u64, _i64, _p],
@@ -234,7 +236,7 @@ def sign_sgd_apply(param, vote_planes, neg_lr, weight_decay, stream=None):
 
 # ----------------------------------------------------------------------- quant
 def dequant_fedavg(tiles, ntiles, nfast, Q, F, sz, rows, weight, total, out, sz_strides=None,
-                   stream=None):
+                   mode=FEDAVG_EXACT, stream=None):
     """nfast: the QTILE_GROUPS counts of grouped tiles at the head of the table
     (quant_store.QuantLayout.tiles()); sz: (scale, zero point) pairs;
     sz_strides = (row, channel) strides in pairs (default: a channel-major
@@ -243,12 +245,12 @@ def dequant_fedavg(tiles, ntiles, nfast, Q, F, sz, rows, weight, total, out, sz_
     nf = (ctypes.c_int32 * QTILE_GROUPS)(*[int(x) for x in nfast])
     if sz_strides is None:
         sz_strides = (sz.stride(1) // 2, sz.stride(0) // 2)
-    _check(lib().dls_dequant_fedavg(_ptr(tiles), ntiles, nf, _ptr(Q),
-                                    Q.stride(0) if Q is not None else 0,
-                                    _ptr(F), F.stride(0) if F is not None else 0, _ptr(sz),
-                                    int(sz_strides[0]), int(sz_strides[1]), _ptr(rows),
-                                    _ptr(weight), rows.numel(), float(total), _ptr(out),
-                                    _stream(stream, out)), "dls_dequant_fedavg")
+    _check(lib().dls_dequant_fedavg_mode(_ptr(tiles), ntiles, nf, _ptr(Q),
+                                         Q.stride(0) if Q is not None else 0,
+                                         _ptr(F), F.stride(0) if F is not None else 0, _ptr(sz),
+                                         int(sz_strides[0]), int(sz_strides[1]), _ptr(rows),
+                                         _ptr(weight), rows.numel(), float(total), int(mode),
+                                         _ptr(out), _stream(stream, out)), "dls_dequant_fedavg")
     return out
 
 

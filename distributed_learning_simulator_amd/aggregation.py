@@ -78,11 +78,18 @@ def union_batch(subsets, n_of_row, device):
 
 
 class ClientUpdateStore:
-    def __init__(self, layout: ParameterLayout, device, capacity=1):
+    """``acquire_range = (lo, hi)``: this process's own clients take rows [lo, hi)
+    only (a fixed block; the sharded Shapley servers all-gather every rank's block
+    into the rest of ``U`` in place); rows outside it may be lent to other
+    ranks' clients and are never put on the free list."""
+
+    def __init__(self, layout: ParameterLayout, device, capacity=1, acquire_range=None):
         self.layout = layout
         self.device = torch.device(device)
         self.U = torch.zeros((max(1, capacity), layout.P), dtype=torch.float32, device=self.device)
-        self._free = list(range(self.U.shape[0]))[::-1]
+        self._range = acquire_range
+        lo, hi = acquire_range if acquire_range is not None else (0, self.U.shape[0])
+        self._free = list(range(lo, hi))[::-1]
         self._lock = threading.Lock()
 
     @property
@@ -92,6 +99,9 @@ class ClientUpdateStore:
     def acquire(self):
         with self._lock:
             if not self._free:
+                if self._range is not None:
+                    raise RuntimeError(f"all {self._range[1] - self._range[0]} rows of this "
+                                       "rank's block are in use")
                 old = self.U
                 new_cap = max(2 * old.shape[0], 1)
                 self.U = torch.zeros((new_cap, self.layout.P), dtype=torch.float32,
@@ -102,7 +112,8 @@ class ClientUpdateStore:
 
     def release(self, row):
         with self._lock:
-            self._free.append(row)
+            if self._range is None or self._range[0] <= row < self._range[1]:
+                self._free.append(row)
 
     def write(self, row, parameter_dict):
         self.layout.copy_into(parameter_dict, self.U[row])
@@ -176,6 +187,81 @@ class ClientUpdateStore:
         return out
 
 
+class SlicedClientUpdateStore:
+    """Client rows stored slice-major for the bit-exact sharded FedAvg exchange
+    (distributed.ShardedFedServer, exchange="alltoall"): the flat row is cut into
+    ``world`` slices of L elements (distributed.slice_bounds) and ``B`` is fp32
+    [world, capacity, L], so slice d of every client this rank holds is ONE
+    contiguous block B[d] — the all-to-all sends straight from the store, one
+    block per peer, with no per-client operation and no staging copy.  A
+    client's dict is written tensor by tensor into its slices (a tensor that
+    straddles a slice boundary is written in pieces); ``views`` returns views of
+    the tensors that lie in one slice and copies of the (at most world - 1)
+    straddling ones."""
+
+    def __init__(self, layout: ParameterLayout, device, capacity, world, L):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.world, self.L = world, L
+        self.B = torch.zeros((world, max(1, capacity), L), dtype=torch.float32, device=self.device)
+        self._free = list(range(self.B.shape[1]))[::-1]
+        self._lock = threading.Lock()
+
+    @property
+    def capacity(self):
+        return self.B.shape[1]
+
+    def acquire(self):
+        with self._lock:
+            if not self._free:
+                old = self.B
+                cap = 2 * old.shape[1]
+                self.B = torch.zeros((self.world, cap, self.L), dtype=torch.float32,
+                                     device=self.device)
+                self.B[:, : old.shape[1]].copy_(old)
+                self._free = list(range(old.shape[1], cap))[::-1]
+            return self._free.pop()
+
+    def release(self, row):
+        with self._lock:
+            self._free.append(row)
+
+    def accepts(self, parameter_dict):
+        return self.layout.matches(parameter_dict)
+
+    def _pieces(self, o, m):
+        """(slice, start in slice, start in tensor, length) of flat range [o, o+m)."""
+        L, out, e = self.L, [], o
+        while e < o + m:
+            s, a = divmod(e, L)
+            n = min(o + m - e, L - a)
+            out.append((s, a, e - o, n))
+            e += n
+        return out
+
+    def write(self, row, parameter_dict):
+        dst, src = [], []
+        for name, m, o in zip(self.layout.names, self.layout.numels, self.layout.offsets):
+            t = parameter_dict[name].detach().reshape(-1)
+            t = t if t.dtype == torch.float32 else t.float()
+            for s, a, b, n in self._pieces(o, m):
+                dst.append(self.B[s, row, a:a + n])
+                src.append(t[b:b + n])
+        torch._foreach_copy_(dst, src, non_blocking=True)
+
+    def views(self, row):
+        out = {}
+        for name, shape, m, o in zip(self.layout.names, self.layout.shapes, self.layout.numels,
+                                     self.layout.offsets):
+            parts = [self.B[s, row, a:a + n] for s, a, _, n in self._pieces(o, m)]
+            out[name] = (parts[0] if len(parts) == 1 else torch.cat(parts)).view(shape)
+        return out
+
+    def row(self, row):
+        """The client's flat row (a copy: its slices are not contiguous)."""
+        return self.B[:, row, :].reshape(-1)[: self.layout.P]
+
+
 class ClientParameters(dict):
     """``self.parameters`` of the reference FedServer, backed by a ClientUpdateStore.
 
@@ -233,6 +319,21 @@ class ClientParameters(dict):
 
     def row_of(self, worker_id):
         return self._rows[worker_id]
+
+    def adopt(self, entries):
+        """Re-register the clients as [(worker_id, n, row)] in that order, for rows
+        the store already holds (the sharded Shapley gather lands every rank's
+        clients in place): no copy; rows this process did not acquire are never
+        released to its free list (ClientUpdateStore.acquire_range)."""
+        rows = {w: r for w, _, r in entries}
+        for w in list(self.keys()):
+            if self._rows[w] != rows.get(w):
+                self.store.release(self._rows[w])
+        dict.clear(self)
+        self._rows = {}
+        for w, n, r in entries:
+            self._rows[w] = r
+            dict.__setitem__(self, w, int(n))
 
     def n_of(self, worker_id):
         return dict.__getitem__(self, worker_id)

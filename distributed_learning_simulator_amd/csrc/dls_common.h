@@ -35,6 +35,8 @@ int check_launch(const char *what);
 // Blocks of `kernel` resident on the whole device at once (occupancy x CUs),
 // for persistent grids; cached per (kernel, device, block, lds).
 int resident_blocks(const void *kernel, int block, size_t lds);
+// Compute units of the current device (cached per device).
+int device_cus();
 // Auxiliary stream number idx (0..63) on `parent`'s device for fork/join inside
 // one C-ABI call (nullptr on error).
 hipStream_t side_stream(hipStream_t parent, int idx);

@@ -61,6 +61,22 @@ int resident_blocks(const void *kernel, int block, size_t lds) {
     return n;
 }
 
+int device_cus() {
+    static std::mutex mu;
+    static std::unordered_map<int, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus < 1)
+        cus = 256;
+    cache[dev] = cus;
+    return cus;
+}
+
 hipStream_t side_stream(hipStream_t parent, int idx) {
     // non-blocking streams per (device, idx), created on first use and kept for the
     // process (the library's launchers fork small concurrent kernels onto it and

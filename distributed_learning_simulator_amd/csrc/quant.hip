@@ -241,13 +241,45 @@ __device__ __forceinline__ void accum16_pk(float (&acc)[16], u32x4 qv, f32x2 sz,
     }
 }
 
+// DLS_FEDAVG_FMA (zero point 0): acc = fma(q, c, acc), c = fl(fl(s * n_i) / N) of
+// the (client, channel): 2 conversions + 1 packed fma per element pair; cz.x
+// holds c (op_sel_hi reads it for both halves).  Two independent pairs per step.
+template <bool SEXT>
+__device__ __forceinline__ void accum16_fma(float (&acc)[16], u32x4 qv, f32x2 cz) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const int k = j & 3;
+        const f32x2 xa = f32x2{byte_val<SEXT>(qv[j >> 2], k), byte_val<SEXT>(qv[j >> 2], k + 1)};
+        const f32x2 xb = f32x2{byte_val<SEXT>(qv[(j >> 2) + 2], k),
+                               byte_val<SEXT>(qv[(j >> 2) + 2], k + 1)};
+        f32x2 ra = f32x2{acc[j], acc[j + 1]}, rb = f32x2{acc[j + 8], acc[j + 9]};
+        asm volatile(
+            "v_pk_fma_f32 %[ra], %[xa], %[cz], %[ra] op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %[rb], %[xb], %[cz], %[rb] op_sel_hi:[1,0,1]"
+            : [ra] "+v"(ra), [rb] "+v"(rb)
+            : [xa] "v"(xa), [xb] "v"(xb), [cz] "v"(cz));
+        acc[j] = ra.x;
+        acc[j + 1] = ra.y;
+        acc[j + 8] = rb.x;
+        acc[j + 9] = rb.y;
+    }
+}
+
+// FMA-mode constant of a (client, channel): fl(fl(s * n_i) / N) (IEEE division,
+// once per chunk and channel)
+__device__ __forceinline__ float fma_coef(float s, float wk, float N) { return (s * wk) / N; }
+
+#ifndef DLS_QUANT_PROBE
+#define DLS_QUANT_PROBE 0  // 1: stream-only timing probe (loads + a xor per dword; wrong output)
+#endif
+
 template <int U, int GN>
 struct QBatch {
     u32x4 qv[U][GN];
     float s[U], z[U], wk[U];
 };
 
-template <bool SIGNED, int G, bool TWO>
+template <bool SIGNED, int G, bool TWO, bool FMA>
 __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8_t *__restrict__ Q,
                                                 const uint32_t (&qoff)[G], int64_t ldq,
                                                 const f32x2 *__restrict__ szc, SzLayout L,
@@ -267,6 +299,45 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8
         nsz = szc[(int64_t)cr.r1 * L.row];  // next chunk (its rows landed a chunk ago)
         cr.advance(rows, w, K, base);
         const int n = min(64, K - base);
+        if constexpr (FMA) {
+            // FMA mode: every client of the chunk with zero point 0 -> one
+            // constant per client, fma(q, c, acc) (else the exact path below)
+            if (__ballot(tsz.y != 0.f && __lane_id() < n) == 0) {
+                const float coef = fma_coef(tsz.x, tw, d.b);
+                constexpr int FU = G > 1 ? kQuantUG : kQuantU;  // clients per batch
+                using FB = QBatch<FU, G>;
+                auto ffetch = [&](int j, u32x4 (&qv)[G], float &c) {
+                    const int64_t r = readlane_i(tr, j);
+                    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                        const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);
+#pragma unroll
+                    for (int g = 0; g < G; ++g)
+                        qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+                    c = readlane_f(coef, j);
+                };
+                auto fstep = [&](const u32x4 (&qv)[G], float c) {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) accum16_fma<SIGNED>(acc[g], qv[g], f32x2{c, c});
+                };
+                chunk_pipeline<FU, FB>(
+                    n,
+                    [&](int j0, FB &bt) {
+#pragma unroll
+                        for (int u = 0; u < FU; ++u) ffetch(j0 + u, bt.qv[u], bt.s[u]);
+                    },
+                    [&](const FB &bt) {
+#pragma unroll
+                        for (int u = 0; u < FU; ++u) fstep(bt.qv[u], bt.s[u]);
+                    },
+                    [&](int j) {
+                        u32x4 qv[G];
+                        float c;
+                        ffetch(j, qv, c);
+                        fstep(qv, c);
+                    });
+                continue;
+            }
+        }
         // one wave-uniform decision per chunk: if every client of the chunk takes
         // the common path (exact fl(z*s) and the fast division), the streaming loop
         // carries that path alone, reading (scale, -fl(z*s)) straight from the table
@@ -581,7 +652,7 @@ __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][1
 // One-channel tiles of up to 4 KiB: slice g of the tile is lanes'
 // 16-element chunks 1024 g + 16 lane; the wave walks the clients once for all
 // its slices (per-client table reads and readlanes amortised over G KiB).
-template <bool SIGNED, int G, bool TWO>
+template <bool SIGNED, int G, bool TWO, bool FMA>
 __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                           int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                           const int32_t *__restrict__ rows,
@@ -597,7 +668,8 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
         // idle lanes load a valid duplicate (loads stay unconditional)
         qoff[g] = (uint32_t)(wt.t.src + (e0 < wt.lenpad ? e0 : wt.lenpad - 16));  // ldq < 4 GiB
     }
-    int_one_channel<SIGNED, G, TWO>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
+    int_one_channel<SIGNED, G, TWO, FMA>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K,
+                                         d);
     store_tile<G>(wt, acc, out);
 }
 
@@ -621,7 +693,7 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
 // lane with each client's payload and the check per client.
 constexpr int kSpanMax = 4;
 
-template <bool SIGNED, int G, bool TWO>
+template <bool SIGNED, int G, bool TWO, bool FMA>
 __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                           int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                           const int32_t *__restrict__ rows,
@@ -680,7 +752,17 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         cr.advance(rows, w, K, base);
         const int n = min(64, K - base);
         bool allfast = false;
-        if (staged) {
+        if (staged && FMA) {
+            // FMA mode: every (client, channel) of the chunk with zero point 0
+            // (symmetric int8) accumulates fma(q, c, acc), c = fl(fl(s * n_i) / N)
+            int ok = 1;
+#pragma unroll
+            for (int c = 0; c < kSpanMax; ++c) {
+                ok &= (int)(c >= span) | (int)(tsz[c].y == 0.f);
+                tab[c][__lane_id()] = f32x2{fma_coef(tsz[c].x, tw, d.b), 0.f};
+            }
+            allfast = __ballot(!ok && __lane_id() < n) == 0;
+        } else if (staged) {
             // every (client, channel) of the chunk on the common path: exact fl(z*s)
             // and the fast division range (always, for symmetric int8)
             int ok = d.fast;
@@ -705,10 +787,19 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
                 b.j = j;
             };
             auto sstep = [&](const SOne &b) {
-                // the lane's (s, -zs): a broadcast LDS read (<= kSpanMax addresses per wave)
+                // the lane's (s, -zs) or FMA constant: a broadcast LDS read (<= kSpanMax
+                // addresses per wave)
 #pragma unroll
-                for (int g = 0; g < G; ++g)
-                    accum16_pk<SIGNED, TWO>(acc[g], b.qv[g], tab[0][toff[g] + b.j], b.wk, d);
+                for (int g = 0; g < G; ++g) {
+                    if constexpr (DLS_QUANT_PROBE == 1) {
+                        acc[g][g] += __uint_as_float((b.qv[g].x ^ b.qv[g].y ^ b.qv[g].z ^ b.qv[g].w) &
+                                                     0x3fffffffu);
+                    } else if constexpr (FMA) {
+                        accum16_fma<SIGNED>(acc[g], b.qv[g], tab[0][toff[g] + b.j]);
+                    } else {
+                        accum16_pk<SIGNED, TWO>(acc[g], b.qv[g], tab[0][toff[g] + b.j], b.wk, d);
+                    }
+                }
             };
             chunk_pipeline_1tail<kLaneUS, SBatch>(
                 n,
@@ -801,19 +892,19 @@ __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][1
     }
 }
 
-template <int G, bool TWO>
+template <int G, bool TWO, bool FMA>
 __global__ __launch_bounds__(kBlock, 1) void k_dequant_fast(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
     const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
-    // one launch per (slice count G, division method): each instance has its own
-    // register budget
+    // one launch per (slice count G, division method, mode): each instance has
+    // its own register budget
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
     if (wt.t.kind == 1)
-        fast_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        fast_tile<true, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
     else
-        fast_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        fast_tile<false, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
 }
 
 // fp32 tensors (biases, norm weights) as their own group: tiles of <= 256
@@ -991,7 +1082,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_small(const dls_qtile *__res
     }
 }
 
-template <int G, bool TWO>
+template <int G, bool TWO, bool FMA>
 __global__ __launch_bounds__(kBlock, 1) void k_dequant_lanes(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
@@ -999,9 +1090,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_dequant_lanes(
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
     if (wt.t.kind == 1)
-        lane_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        lane_tile<true, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
     else
-        lane_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        lane_tile<false, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
@@ -1230,8 +1321,20 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
                                   const int32_t *rows,
                                   const float *weight, int32_t K, float total, float *out,
                                   dls_stream_t stream) {
+    return dls_dequant_fedavg_mode(tiles, ntiles, nfast, Q, ldq, F, ldf, sz, sz_row, sz_chan, rows,
+                                   weight, K, total, DLS_FEDAVG_EXACT, out, stream);
+}
+
+extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
+                                       const int32_t *nfast, const void *Q, int64_t ldq,
+                                       const float *F, int64_t ldf, const float *sz,
+                                       int64_t sz_row, int64_t sz_chan, const int32_t *rows,
+                                       const float *weight, int32_t K, float total, int32_t mode,
+                                       float *out, dls_stream_t stream) {
     DLS_REQUIRE(tiles && nfast && rows && weight && out && sz, DLS_EINVAL,
                 "dls_dequant_fedavg: null pointer");
+    DLS_REQUIRE(mode == DLS_FEDAVG_EXACT || mode == DLS_FEDAVG_FMA, DLS_EINVAL,
+                "dls_dequant_fedavg: mode=%d", mode);
     int64_t nf = 0;
     for (int g = 0; g < DLS_QTILE_GROUPS; ++g) {
         DLS_REQUIRE(nfast[g] >= 0, DLS_EINVAL, "dls_dequant_fedavg: nfast[%d]=%d", g, nfast[g]);
@@ -1251,8 +1354,9 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     DLS_REQUIRE(ldq < ((int64_t)1 << 32), DLS_ELAYOUT,
                 "dls_dequant_fedavg: ldq=%lld must be < 2^32 (32-bit lane offsets)",
                 (long long)ldq);
-    // two-constant division when proven exact for this N, else Markstein
-    const FastDiv d = make_fastdiv2(total);
+    // two-constant division when proven exact for this N, else Markstein (the
+    // FMA-mode bulk kernels divide once per (client, channel) with IEEE '/')
+    const FastDiv d = mode == DLS_FEDAVG_FMA ? make_fastdiv(total) : make_fastdiv2(total);
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
@@ -1297,15 +1401,21 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
     };
     using Kfn = void (*)(const dls_qtile *, int, const uint8_t *, int64_t, const f32x2 *, SzLayout,
                          const int32_t *, const float *, int, FastDiv, float *);
-    static const Kfn kgroup[8][2] = {
-        {k_dequant_fast<4, false>, k_dequant_fast<4, true>},
-        {k_dequant_fast<3, false>, k_dequant_fast<3, true>},
-        {k_dequant_fast<2, false>, k_dequant_fast<2, true>},
-        {k_dequant_fast<1, false>, k_dequant_fast<1, true>},
-        {nullptr, nullptr},  // groups 4-6: rejected above
-        {nullptr, nullptr},
-        {nullptr, nullptr},
-        {k_dequant_lanes<1, false>, k_dequant_lanes<1, true>}};
+    // [group][0: Markstein, 1: two-constant division, 2: FMA mode]
+    static const Kfn kgroup[8][3] = {
+        {k_dequant_fast<4, false, false>, k_dequant_fast<4, true, false>,
+         k_dequant_fast<4, false, true>},
+        {k_dequant_fast<3, false, false>, k_dequant_fast<3, true, false>,
+         k_dequant_fast<3, false, true>},
+        {k_dequant_fast<2, false, false>, k_dequant_fast<2, true, false>,
+         k_dequant_fast<2, false, true>},
+        {k_dequant_fast<1, false, false>, k_dequant_fast<1, true, false>,
+         k_dequant_fast<1, false, true>},
+        {nullptr, nullptr, nullptr},  // groups 4-6: rejected above
+        {nullptr, nullptr, nullptr},
+        {nullptr, nullptr, nullptr},
+        {k_dequant_lanes<1, false, false>, k_dequant_lanes<1, true, false>,
+         k_dequant_lanes<1, false, true>}};
     // A wave walks all K clients, so waves are long and equal: a group is launched
     // in pieces of at most one generation of resident waves (a last generation of
     // a few waves would run alone at latency-bound speed; cf. dls_fedavg_f32).
@@ -1324,7 +1434,7 @@ extern "C" int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const 
                                out);
             return;
         }
-        const Kfn kern = kgroup[g][d.two ? 1 : 0];
+        const Kfn kern = kgroup[g][mode == DLS_FEDAVG_FMA ? 2 : (d.two ? 1 : 0)];
         const int64_t slots = (int64_t)resident_blocks(reinterpret_cast<const void *>(kern), kBlock,
                                                        0) * wpb;
         const int64_t np = (n + slots - 1) / slots;

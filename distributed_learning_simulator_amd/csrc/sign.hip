@@ -132,32 +132,55 @@ struct HSCounter {
     }
 };
 
-// Vote kernel: one wave per block, lane g owns group g (64 parameters) and
-// walks all K clients: one 16-byte [pos, neg] load per client, batches of 8
-// clients double-buffered through the carry-save counters.  The grid is one
-// generation of resident waves sweeping the client rows in step.  Epilogue:
-// the counters are already bit-sliced (bit b of parameter j's count = bit j
-// of word b), so the fp32 sign needs no unpacking: a bit-sliced comparison of
-// the pos / neg counters gives two words (gt, lt) per group.  Those words (or,
-// when the int32 counts are wanted, the 2B counter words) go through LDS and
-// the wave writes its 4096 outputs coalesced, a 16-lane group per 64-parameter
-// group, instead of 64 lanes each scattering 256 bytes.
-constexpr int kVoteBlock = 64;
-constexpr int kVoteG = 4;    // groups per lane on large models (each wave streams G KB per client)
+// Vote kernel: wave w owns the contiguous range of R groups (64 parameters
+// each) [w R, (w+1) R); lane l owns groups w R + l + 64 q, q < G = ceil(R/64),
+// and walks all K clients: one 16-byte [pos, neg] load per client and group,
+// batches of 8 clients through the carry-save counters.  The grid is one
+// generation of resident waves sweeping the client rows in step.  On large
+// models R is chosen so that the chip gets a whole number of waves per CU
+// (kVoteWPC x CUs): every CU then streams the same number of bytes — with
+// R = 256 (682 waves on ResNet-18) a third of the CUs held 3 waves and the rest
+// 2, and the CUs with 3 set the time.  Epilogue: the counters are already
+// bit-sliced (bit b of parameter j's count = bit j of word b), so the fp32 sign
+// needs no unpacking: a bit-sliced comparison of the pos / neg counters gives
+// two words (gt, lt) per group.  Those words (or, when the int32 counts are
+// wanted, the 2B counter words) go through the wave's LDS slice and the wave
+// writes its outputs coalesced, a 16-lane group per 64-parameter group,
+// instead of 64 lanes each scattering 256 bytes.
+constexpr int kVoteWPBMax = 4;  // waves per block
+#ifndef DLS_VOTE_WPC
+#define DLS_VOTE_WPC 4
+#endif
+#ifndef DLS_VOTE_WPB
+#define DLS_VOTE_WPB 4
+#endif
+constexpr int kVoteWPC = DLS_VOTE_WPC;  // waves per CU on large models (0: R = 256 per wave)
+constexpr int kVoteWPB = DLS_VOTE_WPB;
+static_assert(kVoteWPB >= 1 && kVoteWPB <= kVoteWPBMax, "DLS_VOTE_WPB");
+constexpr int kVoteG = 4;    // widest G (registers: single-buffered 8-client batches)
 constexpr int kVoteDbG = 1;  // widest G whose 8-client batches are double-buffered
 
+// LDS is per wave and the epilogue trip counts differ between the waves of a
+// block, so the epilogue synchronises the wave only (LDS ops of one wave
+// execute in order; the fences keep the compiler from moving them).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <int CB, bool ROWS, int G>
 __device__ __forceinline__ void wave_counts(const uint64_t *__restrict__ planes, int64_t ldp,
                                             const int32_t *__restrict__ rows, int K, int64_t g,
-                                            int64_t ngroups, HSCounter<CB> (&cp)[G],
+                                            int64_t gend, HSCounter<CB> (&cp)[G],
                                             HSCounter<CB> (&cn)[G], uint64_t (&nan)[G]) {
-    // lane's groups: g + 64 q, q < G (each load instruction covers 1 KB of a row);
-    // groups past the end re-read group g (in bounds) and are never written
+    // lane's groups: g + 64 q, q < G (each load instruction covers up to 1 KB of
+    // a row); groups past the wave's range (or the model) re-read group g (in
+    // bounds) and are never written
     const u64x2 *base = reinterpret_cast<const u64x2 *>(planes) + g;
     int qoff[G];
 #pragma unroll
-    for (int q = 0; q < G; ++q) qoff[q] = g + 64 * q < ngroups ? 64 * q : 0;
+    for (int q = 0; q < G; ++q) qoff[q] = g + 64 * q < gend ? 64 * q : 0;
     const int64_t ldp2 = ldp / 2;
     constexpr int B8 = 8;
     auto row = [&](int k) -> int64_t { return ROWS ? (int64_t)rows[k] : (int64_t)k; };
@@ -238,36 +261,38 @@ __device__ __forceinline__ void sliced(const HSCounter<CB> &h, uint64_t (&x)[CB 
 }
 
 template <int CB, bool COUNTS, int G>
-__global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__restrict__ planes,
-                                                          int64_t ldp,
-                                                          const int32_t *__restrict__ rows, int K,
-                                                          int64_t P, int64_t ngroups,
-                                                          int32_t *__restrict__ counts,
-                                                          float *__restrict__ sign_out,
-                                                          uint64_t *__restrict__ vote_planes,
-                                                          int64_t vote_groups) {
+__global__ __launch_bounds__(64 * kVoteWPBMax) void k_sign_vote(
+    const uint64_t *__restrict__ planes, int64_t ldp, const int32_t *__restrict__ rows, int K,
+    int64_t P, int64_t ngroups, int32_t *__restrict__ counts, float *__restrict__ sign_out,
+    uint64_t *__restrict__ vote_planes, int64_t vote_groups, int64_t rgroups) {
     constexpr int B = CB + 3;
     constexpr int NW = COUNTS ? 2 * B + 1 : 3;  // words per group through LDS
-    __shared__ uint64_t xw[NW][64];
+    extern __shared__ uint64_t xws[];  // [waves per block][NW][64] (launch: vote_lds)
+    uint64_t(*xw)[64] = reinterpret_cast<uint64_t(*)[64]>(xws + (threadIdx.x >> 6) * NW * 64);
     const int lane = __lane_id();
-    const int64_t gb = (int64_t)blockIdx.x * 64 * G;
+    // the wave's group range [wlo, whi); groups >= ngroups are the zero padding of
+    // the last 256-parameter tile (vote 0)
+    const int64_t wlo = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rgroups;
+    if (wlo >= vote_groups) return;  // wave-uniform
+    const int64_t whi = min(wlo + rgroups, vote_groups);
+    const int64_t gend = min(whi, ngroups);
     HSCounter<CB> cpa[G], cna[G];
     uint64_t nana[G];
 #pragma unroll
     for (int q = 0; q < G; ++q) nana[q] = 0;
-    if (gb + lane < ngroups) {
+    if (wlo + lane < gend) {
         if (rows)
-            wave_counts<CB, true, G>(planes, ldp, rows, K, gb + lane, ngroups, cpa, cna, nana);
+            wave_counts<CB, true, G>(planes, ldp, rows, K, wlo + lane, gend, cpa, cna, nana);
         else
-            wave_counts<CB, false, G>(planes, ldp, rows, K, gb + lane, ngroups, cpa, cna, nana);
+            wave_counts<CB, false, G>(planes, ldp, rows, K, wlo + lane, gend, cpa, cna, nana);
     }
 #pragma unroll
     for (int q = 0; q < G; ++q) {
-        const int64_t g0 = gb + 64 * q;
-        if (g0 >= ngroups && g0 >= vote_groups) break;  // wave-uniform
+        const int64_t g0 = wlo + 64 * q;
+        if (g0 >= whi) break;  // wave-uniform
         const int64_t g = g0 + lane;
         const HSCounter<CB> &cp = cpa[q], &cn = cna[q];
-        const bool live = g < ngroups;  // padding groups (q > 0 lanes re-read group g) vote 0
+        const bool live = g < gend;  // padding groups (q > 0 lanes re-read group g) vote 0
         const uint64_t nan = live ? nana[q] : 0;
         uint64_t xp[B], xn[B];
         sliced<CB>(cp, xp);
@@ -287,7 +312,7 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
         }
         // the vote in the wire format (16 coalesced bytes per lane); NaN-poisoned
         // and tied parameters vote 0 (neither bit)
-        if (vote_planes && g < vote_groups)
+        if (vote_planes && g < whi)
             reinterpret_cast<u64x2 *>(vote_planes)[g] = u64x2{gt & ~nan, lt & ~nan};
         if (COUNTS) {
     #pragma unroll
@@ -302,14 +327,14 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
             xw[2][lane] = nan;
         }
         if (!sign_out && !COUNTS) continue;  // wave-uniform: the packed vote was all
-        __syncthreads();
+        wave_sync();
         // a 16-lane group writes one group's 64 parameters, 4 per lane
         const int jb = 4 * (lane & 15);
     #pragma unroll 4
         for (int it = 0; it < 16; ++it) {
             const int gl = it * 4 + (lane >> 4);
             const int64_t e = (g0 + gl) * 64 + jb;
-            if (e >= P) continue;  // P % 4 == 0: all four or none
+            if (g0 + gl >= whi || e >= P) continue;  // P % 4 == 0: all four or none
             f32x4 s4;
             if (COUNTS) {
                 int pc[4] = {0, 0, 0, 0}, nc[4] = {0, 0, 0, 0};
@@ -346,7 +371,7 @@ __global__ __launch_bounds__(kVoteBlock) void k_sign_vote(const uint64_t *__rest
             }
             if (sign_out) *reinterpret_cast<f32x4 *>(sign_out + e) = s4;
         }
-        __syncthreads();  // xw is rewritten for the next q
+        wave_sync();  // xw is rewritten for the next q
     }
 }
 
@@ -460,19 +485,50 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
                 int32_t *counts, float *sign_out, uint64_t *vote_planes, hipStream_t st) {
     const int64_t ngroups = (P + 63) / 64;
     const int64_t vote_groups = DLS_SIGN_WORDS(P) / 2;  // whole 256-parameter tiles
-    // 4 groups per lane (each wave streams 4 KB of every client row, measured
-    // 12 % faster than 1 KB at P = 11.2M) while that still leaves >= 2 waves per
-    // CU; 1 group per lane (double-buffered batches) for small models
-    constexpr int GW = kVoteG;
-    const bool wide = CB <= 12 && (vote_groups + 64 * GW - 1) / (64 * GW) >= 512;
-    const dim3 grid((unsigned)(wide ? (vote_groups + 64 * GW - 1) / (64 * GW) : (vote_groups + 63) / 64));
-#define DLS_VOTE_LAUNCH(C_, G_)                                                              \
-    hipLaunchKernelGGL((k_sign_vote<CB, C_, G_>), grid, dim3(kVoteBlock), 0, st, planes, ldp, \
-                       rows, K, P, ngroups, counts, sign_out, vote_planes, vote_groups)
-    if (counts && wide) DLS_VOTE_LAUNCH(true, GW);
-    else if (counts) DLS_VOTE_LAUNCH(true, 1);
-    else if (wide) DLS_VOTE_LAUNCH(false, GW);
-    else DLS_VOTE_LAUNCH(false, 1);
+    // Large models: kVoteWPC waves per CU, each a contiguous range of R groups,
+    // 2-4 groups per lane (each wave streams R x 16 B of every client row:
+    // multi-KB pieces measured 12 % faster than 1 KB at P = 11.2M).  Small
+    // models: R = 64, 1 group per lane, double-buffered batches.
+    int64_t R = 64;
+    int G = 1, wpb = 1;
+    if (CB <= 12) {
+        if (kVoteWPC > 0) {
+            const int64_t waves = (int64_t)kVoteWPC * device_cus();
+            const int64_t r = (vote_groups + waves - 1) / waves;
+            if (r > 64 && r <= 64 * kVoteG) {
+                R = r;
+                G = (int)((r + 63) / 64);
+                wpb = kVoteWPB;
+            }
+        } else if ((vote_groups + 64 * kVoteG - 1) / (64 * kVoteG) >= 512) {
+            R = 64 * kVoteG;  // the round-3 form: 256 groups per wave, one wave per block
+            G = kVoteG;
+        }
+    }
+    const int64_t nwaves = (vote_groups + R - 1) / R;
+    const dim3 grid((unsigned)((nwaves + wpb - 1) / wpb));
+    const size_t lds = (size_t)wpb * (counts ? 2 * (CB + 3) + 1 : 3) * 64 * sizeof(uint64_t);
+#define DLS_VOTE_LAUNCH(C_, G_)                                                                  \
+    hipLaunchKernelGGL((k_sign_vote<CB, C_, G_>), grid, dim3(64 * wpb), lds, st, planes, ldp, rows, \
+                       K, P, ngroups, counts, sign_out, vote_planes, vote_groups, R)
+#define DLS_VOTE_BY_G(C_)                     \
+    switch (G) {                              \
+        case 1: DLS_VOTE_LAUNCH(C_, 1); break; \
+        case 2: DLS_VOTE_LAUNCH(C_, 2); break; \
+        case 3: DLS_VOTE_LAUNCH(C_, 3); break; \
+        default: DLS_VOTE_LAUNCH(C_, 4); break; \
+    }
+    if constexpr (CB > 12) {  // wide counters: 1 group per lane only (registers)
+        if (counts) DLS_VOTE_LAUNCH(true, 1);
+        else DLS_VOTE_LAUNCH(false, 1);
+    } else {
+        if (counts) {
+            DLS_VOTE_BY_G(true)
+        } else {
+            DLS_VOTE_BY_G(false)
+        }
+    }
+#undef DLS_VOTE_BY_G
 #undef DLS_VOTE_LAUNCH
     return check_launch("dls_sign_vote");
 }

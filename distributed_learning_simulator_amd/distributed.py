@@ -15,8 +15,10 @@ collective combines the ranks:
   within a shard, cross-rank sums in RCCL order: normwise ~1e-7 vs the exact
   mean (north-star tolerance 1e-6), not bit-exact.
   ``ShardedFedServer(exchange="alltoall")`` is the bit-exact alternative:
-  parameter slices per rank, one all-to-all of the client rows, the
-  reference-order kernel over all clients on each slice, one all-gather.
+  parameter slices per rank, the client rows stored slice-major so that ONE
+  ``all_to_all_single`` moves every client's slice to its owner straight from
+  the store, the reference-order kernel over all clients on each slice, one
+  all-gather.
 * sign vote: int32 vote counts per rank, SUM all-reduce, then sign on every
   rank — bit-exact for any number of ranks.
 
@@ -134,7 +136,11 @@ class ShardedFedServer(_ShardedMixin, FedServer):
     reference's: ``self.parameters.keys()`` in insertion order,
     servers/fed_server.py:69-73,81) merges the ranks' arrivals by the
     node-wide monotonic clock at which each update reached its rank's queue
-    thread (ties by worker id); ``"worker_id"`` sorts by id."""
+    thread (ties by worker id) — the reference's order, and like the
+    reference's it depends on thread timing, so two runs can give different
+    bits; the clock is only comparable within one node, so when the ranks span
+    several hosts the server falls back to ``"worker_id"`` (with a warning).
+    ``"worker_id"`` sorts by id: the same bits on every run."""
 
     def __init__(self, group=None, chunks=3, exchange="allreduce", order="arrival", **kwargs):
         if exchange not in ("allreduce", "alltoall"):
@@ -146,7 +152,27 @@ class ShardedFedServer(_ShardedMixin, FedServer):
         self._arrival = {}
         self._clock = time.monotonic_ns  # system-wide on Linux: comparable across ranks
         self._init_shard(kwargs["worker_number"], group, chunks)
+        if exchange == "alltoall" and order == "arrival" and self.world_size > 1:
+            import socket
+            hosts = [None] * self.world_size
+            dist.all_gather_object(hosts, socket.gethostname(), group=group)
+            if len(set(hosts)) > 1:
+                import logging
+                logging.getLogger("distributed_learning_simulator_amd").warning(
+                    "order='arrival' needs one node's monotonic clock; ranks span %d hosts, "
+                    "summing in worker-id order", len(set(hosts)))
+                self.order = "worker_id"
         super().__init__(**kwargs)
+
+    def _make_store(self, parameter_dict):
+        if self.exchange != "alltoall":
+            return super()._make_store(parameter_dict)
+        from .aggregation import SlicedClientUpdateStore
+        from .layout import ParameterLayout
+        layout = ParameterLayout.from_dict(parameter_dict)
+        bounds = slice_bounds(layout.P, self.world_size)
+        return SlicedClientUpdateStore(layout, self.device, self.store_capacity, self.world_size,
+                                       bounds[1] - bounds[0])
 
     def _process_worker_data(self, data, __):
         wid = data[0]
@@ -158,69 +184,63 @@ class ShardedFedServer(_ShardedMixin, FedServer):
         return result
 
     def _global_order(self, ids):
-        """[(worker_id, n, home rank)] of every rank's clients in summation order."""
+        """[(worker_id, n, home rank, row in home's store)] of every rank's clients
+        in summation order, and every rank's store capacity."""
         dev, world = self.device, self.world_size
         kmax = max(1, -(-self.worker_number // world))  # >= any rank's local clients
-        meta = [[int(wid), self.parameters.n_of(wid), self._arrival.get(wid, 0)] for wid in ids]
-        meta += [[-1, 0, 0]] * (kmax - len(meta))
+        cap = self.parameters.store.capacity
+        meta = [[int(wid), self.parameters.n_of(wid), self._arrival.get(wid, 0),
+                 self.parameters.row_of(wid), cap] for wid in ids]
+        meta += [[-1, 0, 0, 0, cap]] * (kmax - len(meta))
         meta = torch.tensor(meta, dtype=torch.int64).to(dev)  # one host -> device copy
-        metas = torch.empty((world * kmax, 3), dtype=torch.int64, device=dev)
+        metas = torch.empty((world * kmax, 5), dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(metas, meta, group=self.group)
-        entries = [(t, wid, n, i // kmax) for i, (wid, n, t) in enumerate(metas.tolist())
+        metas = metas.tolist()
+        caps = [metas[r * kmax][4] for r in range(world)]
+        entries = [(t, wid, n, i // kmax, row) for i, (wid, n, t, row, _) in enumerate(metas)
                    if wid >= 0]
         if self.order == "worker_id":
             entries.sort(key=lambda e: e[1])
         else:
             entries.sort(key=lambda e: (e[0], e[1]))
-        return [(wid, n, home) for _, wid, n, home in entries]
+        return [(wid, n, home, row) for _, wid, n, home, row in entries], caps
 
     def _bitexact_mean(self, ids):
-        """exchange="alltoall": the mean of every rank's clients, bit-exact."""
+        """exchange="alltoall": the mean of every rank's clients, bit-exact.
+
+        The store is slice-major (SlicedClientUpdateStore: B [world, capacity, L]),
+        so ONE all_to_all_single sends block B[d] — slice d of every client this
+        rank holds — to rank d, straight from the store, and lands every rank's
+        block for my slice in ``recv`` [sum of capacities, L]; the kernel then
+        walks those rows in the summation order (row indices, no gather)."""
         store = self.parameters.store
         P, dev, world, me = store.layout.P, self.device, self.world_size, self.rank
-        order = self._global_order(ids)
-        bounds = slice_bounds(P, world)
-        L = bounds[1] - bounds[0]
-        mine = bounds[me + 1] - bounds[me]
-        # recv[i]: my slice of the i-th client of the summation order; my own
-        # clients' slices are copied out of the store (1/world of my rows), every
-        # other rank's arrive point-to-point from its store rows
-        recv = torch.empty((len(order), max(mine, 4)), dtype=torch.float32, device=dev)
-        staged = dist.get_backend(self.group) == "gloo" and recv.is_cuda  # gloo: host tensors
-        ops, landing = [], []
-        for i, (wid, _, home) in enumerate(order):
-            if home == me:
-                row = store.row(self.parameters.row_of(wid))
-                recv[i, :mine].copy_(row[bounds[me]:bounds[me] + mine])
-                for d in range(world):
-                    n_d = bounds[d + 1] - bounds[d]
-                    if d == me or n_d == 0:
-                        continue
-                    src = row[bounds[d]:bounds[d + 1]]
-                    ops.append(dist.P2POp(dist.isend, src.cpu() if staged else src,
-                                          self._peer(d)))
-            elif mine > 0:
-                dst = recv[i, :mine]
-                if staged:
-                    host = torch.empty(mine, dtype=torch.float32)
-                    landing.append((dst, host))
-                    dst = host
-                ops.append(dist.P2POp(dist.irecv, dst, self._peer(home)))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        for dst, host in landing:
-            dst.copy_(host)
-        total = sum(n for _, n, _ in order)
+        order, caps = self._global_order(ids)
+        L = store.L
+        mine = slice_bounds(P, world)[me + 1] - slice_bounds(P, world)[me]
+        base = [0]
+        for c in caps:
+            base.append(base[-1] + c)
+        recv = torch.empty((base[-1], L), dtype=torch.float32, device=dev)
+        send = store.B.view(-1)
+        in_splits = [store.capacity * L] * world
+        out_splits = [c * L for c in caps]
+        if dist.get_backend(self.group) == "gloo" and recv.is_cuda:  # gloo: host tensors
+            rh = torch.empty(recv.shape, dtype=torch.float32)
+            dist.all_to_all_single(rh.view(-1), send.cpu(), out_splits, in_splits, group=self.group)
+            recv.copy_(rh)
+        else:
+            dist.all_to_all_single(recv.view(-1), send, out_splits, in_splits, group=self.group)
+        total = sum(n for _, n, _, _ in order)
         part = torch.zeros(L, dtype=torch.float32, device=dev)
         if mine > 0:  # a rank whose slice is empty (P < 64 * world) only joins the gather
-            from .aggregation import _f32
+            from .aggregation import _f32, _i32
             from .servers.fed_server import _MODES
-            _native.fedavg(recv, torch.arange(len(order), dtype=torch.int32, device=dev),
-                           _f32([n for _, n, _ in order], dev), float(total), mine, part,
-                           mode=_MODES[self.aggregation_mode])
+            rows = _i32([base[home] + row for _, _, home, row in order], dev)
+            _native.fedavg(recv, rows, _f32([n for _, n, _, _ in order], dev), float(total), mine,
+                           part, mode=_MODES[self.aggregation_mode])
         out = torch.empty(world * L, dtype=torch.float32, device=dev)
-        if staged:
+        if dist.get_backend(self.group) == "gloo" and part.is_cuda:
             oh = torch.empty(world * L, dtype=torch.float32)
             dist.all_gather_into_tensor(oh, part.cpu(), group=self.group)
             out.copy_(oh)
@@ -329,45 +349,49 @@ class ShardedSignSGDServer(SignSGDServer):
 
 class _ShardedShapleyMixin(_ShardedMixin):
     """Shapley servers on several ranks: each rank receives its own
-    clients' updates, one all-gather per round gives every rank all K client rows
-    (RCCL over xGMI), then the coalitions of every evaluation batch are dealt
-    round-robin over the ranks (``ShapleyValueServer.evaluate_subsets``)."""
+    clients' updates into its own block of rows of the store (rows
+    [rank * kmax, (rank + 1) * kmax) of U [world * kmax, P]), one in-place
+    ``all_gather_into_tensor`` per round fills every other block (RCCL over
+    xGMI, no staging copy), the arrived rows are registered without a copy, and
+    the coalitions of every evaluation batch are dealt round-robin over the
+    ranks (``ShapleyValueServer.evaluate_subsets``)."""
+
+    @property
+    def _kmax(self):
+        return max(1, -(-self.worker_number // self.world_size))
+
+    def _make_store(self, parameter_dict):
+        from .aggregation import ClientUpdateStore
+        from .layout import ParameterLayout
+        k = self._kmax
+        return ClientUpdateStore(ParameterLayout.from_dict(parameter_dict), self.device,
+                                 capacity=self.world_size * k,
+                                 acquire_range=(self.rank * k, (self.rank + 1) * k))
 
     def _gather_clients(self):
         store = self.parameters.store
-        P = store.layout.P
+        k, me, world = self._kmax, self.rank, self.world_size
         local = list(self.parameters.keys())
-        kmax = max(1, -(-self.worker_number // self.world_size))
-        buf = torch.zeros((kmax, P), dtype=torch.float32, device=self.device)
-        for j, wid in enumerate(local):
-            buf[j].copy_(store.row(self.parameters.row_of(wid)))
-        # built on the host, one host -> device copy
-        meta = [[int(wid), self.parameters.n_of(wid)] for wid in local]
-        meta += [[-1, 0]] * (kmax - len(meta))
+        # (worker id, n, row) of the local clients, built on the host, one copy
+        meta = [[int(w), self.parameters.n_of(w), self.parameters.row_of(w)] for w in local]
+        meta += [[-1, 0, 0]] * (k - len(meta))
         meta = torch.tensor(meta, dtype=torch.int64).to(self.device)
-        bufs = [torch.empty_like(buf) for _ in range(self.world_size)]
-        metas = [torch.empty_like(meta) for _ in range(self.world_size)]
-        dist.all_gather(bufs, buf, group=self.group)
-        dist.all_gather(metas, meta, group=self.group)
-        incoming = {}
-        for b, m in zip(bufs, metas):
-            for j, (wid, n) in enumerate(m.tolist()):
-                if wid >= 0:
-                    incoming[wid] = (n, b[j])
-        # every rank now holds all K clients, in worker-id order
-        for wid in list(self.parameters.keys()):
-            del self.parameters[wid]
-        for wid in sorted(incoming):
-            n, row = incoming[wid]
-            self.parameters[wid] = (n, store.layout.views(row))
+        metas = torch.empty((world * k, 3), dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(metas, meta, group=self.group)
+        U = store.U[: world * k]
+        mine = store.U[me * k:(me + 1) * k]
+        if dist.get_backend(self.group) == "gloo":  # gloo: host tensors, no in-place aliasing
+            uh = torch.empty(U.shape, dtype=torch.float32)
+            dist.all_gather_into_tensor(uh, mine.cpu().clone(), group=self.group)
+            U.copy_(uh)
+        else:  # in place: rank r's block is its input (RCCL's in-place all-gather)
+            dist.all_gather_into_tensor(U, mine, group=self.group)
+        # every rank now holds all K clients, registered in worker-id order
+        entries = sorted((w, n, row) for w, n, row in metas.tolist() if w >= 0)
+        self.parameters.adopt(entries)
 
     def _before_aggregate(self):
         self._gather_clients()
-
-    @property
-    def store_capacity(self):
-        return self.worker_number  # every rank ends the round holding all K client rows
-
 
 def _sharded_shapley(cls):
     class Sharded(_ShardedShapleyMixin, cls):

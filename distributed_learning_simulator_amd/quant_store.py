@@ -231,7 +231,9 @@ class QuantizedClientStore:
                 self.F[row, ql.src[i]:ql.src[i] + n].copy_(v.reshape(-1).float(),
                                                            non_blocking=True)
 
-    def fedavg(self, rows, ns, out=None, total=None):
+    def fedavg(self, rows, ns, out=None, total=None, mode=_native.FEDAVG_EXACT):
+        """Dequant + weighted mean of the rows (dls_dequant_fedavg_mode): EXACT is
+        bit-exact with the reference's dequant-then-average, FMA within 1e-6."""
         if out is None:
             out = torch.empty(self.layout.P, dtype=torch.float32, device=self.device)
         if total is None:
@@ -239,7 +241,7 @@ class QuantizedClientStore:
         rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
         w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
         _native.dequant_fedavg(self.tiles, self.ntiles, self.nfast, self.Q, self.F, self.sz,
-                               rows_t, w_t, float(total), out)
+                               rows_t, w_t, float(total), out, mode=mode)
         return out
 
     def dequantize(self, row):

@@ -12,8 +12,10 @@ After aggregation the reference calls the absent library's
 ``stochastic_quantization(256)`` on the concatenated aggregate (:35-39) and
 returns a ``(quantized_pair, dequant)`` tuple that ``FedServer`` then tries to
 load as a parameter dict (D4, broken).  This build's contract instead:
-per named tensor, MinMax affine 8-bit quantization on the GPU (segment min/max
--> qparams -> quantize, all ``libdls_hip``), deterministic by default
+MinMax affine 8-bit quantization on the GPU (segment min/max -> qparams ->
+quantize, all ``libdls_hip``) over the concatenated aggregate like the
+reference's call site (``granularity="model"``, default) or per named tensor
+(``granularity="tensor"``), deterministic by default
 (``stochastic=True`` switches to seeded stochastic rounding — parity unpinned);
 the broadcast is the dequantized model and ``self.quantized_parameter`` holds
 the (q uint8, scale, zero_point) wire payload.  The reference's stale
@@ -26,20 +28,39 @@ import torch
 from .. import _native
 from ..model_util import get_data_serialization_size
 from ..quant_store import QuantizedClientStore
-from .fed_server import FedServer
+from .fed_server import _MODES, FedServer
 
 log = logging.getLogger("distributed_learning_simulator_amd")
 
 
 class FedQuantServer(FedServer):
-    def __init__(self, quantization_level=256, stochastic=False, seed=0, **kwargs):
+    """``granularity`` of the re-quantization of the aggregate:
+
+    * ``"model"`` (default, the reference's): one quantizer over the whole
+      flattened aggregate, as ``quant(concat_dict_values(aggregated_parameter))``
+      (servers/fed_quant_server.py:39) — one (scale, zero point) pair, and the
+      wire payload's q is the concatenation of every tensor's bytes in dict order;
+    * ``"tensor"``: one (scale, zero point) pair per named tensor, q in the
+      store's flat layout (tensors 64-element aligned).
+
+    ``aggregation_mode="fma"`` runs the fused dequant-FedAvg with one constant per
+    (client, channel) (dls_dequant_fedavg_mode, DLS_FEDAVG_FMA: within the
+    north-star 1e-6 FedAvg tolerance, not bit-exact); the default "exact" is
+    bit-exact with the reference's dequant-then-average."""
+
+    def __init__(self, quantization_level=256, stochastic=False, seed=0, granularity="model",
+                 **kwargs):
+        if granularity not in ("model", "tensor"):
+            raise ValueError(f"granularity must be 'model' or 'tensor', not {granularity!r}")
         super().__init__(**kwargs)
         self.parameter = None
         self.quantization_level = quantization_level  # servers/fed_quant_server.py:37
         self.stochastic = stochastic
         self.seed = seed
+        self.granularity = granularity
         self.quantized_parameter = None
         self.last_aggregate = None
+        self._compact_index = None
 
     def _make_store(self, payload):
         return QuantizedClientStore(payload, self.device, capacity=self.store_capacity)
@@ -50,7 +71,16 @@ class FedQuantServer(FedServer):
         return client_parameter
 
     def _aggregate(self, store, rows, ns, total=None):
-        return store.fedavg(rows, ns, total=total)
+        return store.fedavg(rows, ns, total=total, mode=_MODES[self.aggregation_mode])
+
+    def _compact(self, layout, q):
+        """The real elements of a flat-layout row, concatenated in dict order
+        (concat_dict_values): one gather with a cached index."""
+        if self._compact_index is None or self._compact_index.device != q.device:
+            idx = torch.cat([torch.arange(o, o + m, dtype=torch.int64)
+                             for o, m in zip(layout.offsets, layout.numels)])
+            self._compact_index = idx.to(q.device)
+        return q.index_select(0, self._compact_index)
 
     def _process_aggregated_parameter(self, aggregated_parameter: dict):
         log.info("begin quantization")
@@ -65,14 +95,29 @@ class FedQuantServer(FedServer):
         mins = torch.empty(T, dtype=torch.float32, device=dev)
         maxs = torch.empty(T, dtype=torch.float32, device=dev)
         _native.segment_minmax(flat, seg, layout.P, mins, maxs)
-        scale = torch.empty(T, dtype=torch.float32, device=dev)
-        zp = torch.empty(T, dtype=torch.int32, device=dev)
-        _native.qparams_minmax(mins, maxs, scale, zp, 0, self.quantization_level - 1)
+        qmax = self.quantization_level - 1
+        if self.granularity == "model":
+            # one quantizer over the concatenated aggregate: the min / max of every
+            # tensor's (the zero row padding only adds 0, which the MinMax qparams
+            # include anyway: min(lo, 0), max(hi, 0))
+            lo = torch.amin(mins, 0, keepdim=True)
+            hi = torch.amax(maxs, 0, keepdim=True)
+            scale1 = torch.empty(1, dtype=torch.float32, device=dev)
+            zp1 = torch.empty(1, dtype=torch.int32, device=dev)
+            _native.qparams_minmax(lo, hi, scale1, zp1, 0, qmax)
+            scale, zp = scale1.expand(T).contiguous(), zp1.expand(T).contiguous()
+        else:
+            scale = torch.empty(T, dtype=torch.float32, device=dev)
+            zp = torch.empty(T, dtype=torch.int32, device=dev)
+            _native.qparams_minmax(mins, maxs, scale, zp, 0, qmax)
         q = torch.empty(layout.P, dtype=torch.uint8, device=dev)
         deq = torch.empty(layout.P, dtype=torch.float32, device=dev)
         _native.quantize_u8(flat, seg, layout.P, scale, zp, q, deq, stochastic=self.stochastic,
                             seed=self.seed + self.round)
-        self.quantized_parameter = (q, scale, zp)
+        if self.granularity == "model":
+            self.quantized_parameter = (self._compact(layout, q), scale1, zp1)
+        else:
+            self.quantized_parameter = (q, scale, zp)
         # serialized sizes, as the reference's call site (:41-42)
         parameter_size = get_data_serialization_size(aggregated_parameter)
         quantized_parameter_size = get_data_serialization_size(self.quantized_parameter)

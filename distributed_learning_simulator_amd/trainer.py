@@ -10,7 +10,9 @@ of ``optimizer.step()`` when registered (workers/sign_sgd_worker.py:15-17) and
 ``loss_metric.get_loss(1)`` (servers/fed_server.py:26-32).  Local training is
 outside the hot path; this is the plumbing config 1 needs.
 """
+import contextlib
 import enum
+import threading
 
 import torch
 
@@ -42,33 +44,113 @@ class _Loss:
         return self.value
 
 
+_flags_lock = threading.Lock()
+_flags_depth = 0
+_flags_saved = None
+
+
+@contextlib.contextmanager
+def _deterministic_convs():
+    """torch.backends.cudnn.deterministic = True, benchmark = False (MIOpen: only
+    deterministic convolution solutions) while any inference runs; the previous
+    values come back when the last one ends (nested / concurrent testers share
+    one save)."""
+    global _flags_depth, _flags_saved
+    cudnn = torch.backends.cudnn
+    with _flags_lock:
+        if _flags_depth == 0:
+            _flags_saved = (cudnn.deterministic, cudnn.benchmark)
+            cudnn.deterministic, cudnn.benchmark = True, False
+        _flags_depth += 1
+    try:
+        yield
+    finally:
+        with _flags_lock:
+            _flags_depth -= 1
+            if _flags_depth == 0:
+                cudnn.deterministic, cudnn.benchmark = _flags_saved
+
+
 class Inferencer:
     """The tester (ref servers/fed_server.py:26-32): top-1 accuracy / mean loss of
     ``model`` over ``dataset``.
 
+    The utility of a coalition must be a function of the coalition: GTG's
+    truncation tests (servers/GTG_shapley_value_server.py:29,54) and the client
+    ranking compare utilities, and on several GPUs a coalition's utility must not
+    depend on which rank evaluated it.  MIOpen's default convolution algorithms
+    are not run-to-run reproducible on this stack (the 512-channel layers of
+    ResNet-18 gave different bits for the same input), so the GPU forward runs
+    with ``torch.backends.cudnn.deterministic = True, benchmark = False``
+    (``deterministic``, default on): MIOpen then only selects deterministic
+    convolution solutions.  Those are torch's process-wide switches, set for the
+    duration of ``inference()`` / ``logits()`` and restored after it (worker
+    threads that train meanwhile also get deterministic convolutions; their
+    results stay correct).
+
     Models that have a ``forward_fused`` eval path (models.ResNet18) run it on the
     GPU (``fused_eval``, default on): every batch norm + ReLU (+ residual add) as
-    one hand-written NHWC pass (dls_bn_act_exact_nhwc_f32) with the batch-norm
-    library's own arithmetic, ~1.8x faster utility evaluations whose logits are
-    bit-identical to the module's forward (tests/test_gpu_infer.py), so Shapley
-    utilities are those of the plain PyTorch-ROCm model either way.
-    ``fused_eval=False`` runs the module's forward."""
+    one hand-written NHWC pass (dls_bn_act_exact_nhwc_f32) that reproduces the
+    eval batch norm torch runs on this stack (MIOpen's inference kernel); with
+    deterministic convolutions the logits are bit-identical to the module's
+    forward (tests/test_gpu_infer.py).  That equality is a property of this
+    torch / MIOpen build, so every Inferencer checks it once, on its model's
+    first batch norm against ``bn(x)``; if the bits differ it runs the module's
+    forward instead.  ``fused_eval=False`` always runs the module's forward."""
 
-    def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True):
+    def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True,
+                 deterministic=True):
         self.model = model
         self.fused_eval = fused_eval
+        self.deterministic = deterministic
         self.dataset = dataset
         self.batch_size = batch_size
         self.device = device or next(model.parameters()).device
         self.accuracy_metric = _Accuracy()
         self.loss_metric = _Loss()
+        self._fused_checked = None  # None: not yet checked; else the check's verdict
 
     def set_device(self, device):
         self.device = torch.device(device)
         self.model.to(self.device)
 
-    @torch.no_grad()
-    def inference(self):
+    def _flags(self):
+        if not self.deterministic or torch.device(self.device).type != "cuda":
+            return contextlib.nullcontext()
+        return _deterministic_convs()
+
+    def _fused_matches_module(self):
+        """One eval batch norm of the model through the fused pass vs ``bn(x)`` on a
+        small channels_last activation: True when the bits agree."""
+        from . import _native
+        bn = next((m for m in self.model.modules() if isinstance(m, torch.nn.BatchNorm2d)), None)
+        if bn is None:
+            return True
+        g = torch.Generator().manual_seed(0)
+        x = (torch.randn(2, bn.num_features, 5, 5, generator=g) * 3).to(self.device)
+        x = x.contiguous(memory_format=torch.channels_last)
+        consts = torch.empty(4 * bn.num_features, device=self.device)
+        _native.bn_fold_exact(bn, consts)
+        y = _native.bn_act_exact_nhwc(x, consts, relu=False)
+        return torch.equal(y.view(torch.int32), bn(x).view(torch.int32))
+
+    def _fused_forward(self, X):
+        if not (self.fused_eval and X.dim() == 4 and torch.device(self.device).type == "cuda"):
+            return None
+        fused = getattr(self.model, "forward_fused", None)
+        if fused is None:
+            return None
+        if self._fused_checked is None:
+            self._fused_checked = self._fused_matches_module()
+            if not self._fused_checked:
+                import logging
+                logging.getLogger("distributed_learning_simulator_amd").warning(
+                    "fused eval batch norm differs from the module's on this stack; "
+                    "running the module's forward")
+        return fused if self._fused_checked else None
+
+    def _batches(self):
+        """Logits of every batch, in order (the model in eval mode)."""
         X, y = self.dataset
         self.model.eval()
         if X.dim() == 4 and torch.device(self.device).type == "cuda":
@@ -77,24 +159,33 @@ class Inferencer:
             self.model.to(memory_format=torch.channels_last)
         # a model with a fused eval forward (models.ResNet18): every batch norm + ReLU
         # (+ residual add) is one hand-written NHWC pass instead of three kernels
-        fused = (getattr(self.model, "forward_fused", None)
-                 if self.fused_eval and X.dim() == 4 and torch.device(self.device).type == "cuda"
-                 else None)
+        fused = self._fused_forward(X)
         fold = self.model.fold_bn() if fused is not None else None
-        correct = torch.zeros((), dtype=torch.int64, device=self.device)
-        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         for i in range(0, X.shape[0], self.batch_size):
             xb = X[i:i + self.batch_size].to(self.device, non_blocking=True)
             yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
             if xb.dim() == 4 and xb.is_cuda:
                 xb = xb.contiguous(memory_format=torch.channels_last)
-            out = fused(xb, fold) if fused is not None else self.model(xb)
-            loss_sum += torch.nn.functional.cross_entropy(out, yb, reduction="sum").double()
-            correct += (out.argmax(1) == yb).sum()
-        n = X.shape[0]
-        # one host synchronisation per evaluation instead of two per batch
-        self.accuracy_metric.value = int(correct) / n
-        self.loss_metric.value = torch.tensor(float(loss_sum) / n)
+            yield (fused(xb, fold) if fused is not None else self.model(xb)), yb
+
+    @torch.no_grad()
+    def logits(self):
+        """The logits ``inference()`` scores, concatenated over the dataset."""
+        with self._flags():
+            return torch.cat([out for out, _ in self._batches()])
+
+    @torch.no_grad()
+    def inference(self):
+        with self._flags():
+            correct = torch.zeros((), dtype=torch.int64, device=self.device)
+            loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+            for out, yb in self._batches():
+                loss_sum += torch.nn.functional.cross_entropy(out, yb, reduction="sum").double()
+                correct += (out.argmax(1) == yb).sum()
+            n = self.dataset[0].shape[0]
+            # one host synchronisation per evaluation instead of two per batch
+            self.accuracy_metric.value = int(correct) / n
+            self.loss_metric.value = torch.tensor(float(loss_sum) / n)
         return self.loss_metric.value, self.accuracy_metric.value, None
 
 

@@ -70,37 +70,44 @@ def fake_quantize_per_channel_symmetric(w):
     return q.float() * scale.view(-1, *([1] * (w.dim() - 1)))
 
 
+def _fake_quant_pre_hook(mod, args):
+    w = mod._parameters["weight"]
+    object.__setattr__(mod, "_dls_fq_weight", w)  # a plain attribute, not a registered Parameter
+    mod._parameters["weight"] = _StraightThrough.apply(w, fake_quantize_per_channel_symmetric(w))
+
+
+def _fake_quant_post_hook(mod, args, output):
+    w = mod.__dict__.pop("_dls_fq_weight", None)
+    if w is not None:
+        mod._parameters["weight"] = w
+
+
 class WeightFakeQuant:
     """QAT: each module owning a weight Parameter with dim >= 2 (conv, linear)
     sees ``_StraightThrough(w, fake_quant(w))`` as its weight during its forward;
     the Parameter itself (and the optimizer's reference) is unchanged, and it is
-    back in place when the forward returns or raises (the module's forward is
-    wrapped in try/finally, so named_parameters() / state_dict() / .to() never
-    see the fake-quantized tensor)."""
+    back in place when the forward returns or raises: a forward pre-hook swaps
+    it in and a forward hook registered with ``always_call=True`` swaps it back,
+    so named_parameters() / state_dict() / .to() never see the fake-quantized
+    tensor.  The hooks are module-level functions that act on the module they
+    are called with, so a deep copy of the model (``Trainer.get_inferencer(
+    copy_model=True)``) fake-quantizes its own weights, and the model pickles."""
 
     def __init__(self, model):
         self.modules = []
+        self._handles = []
         for mod in model.modules():
             w = mod._parameters.get("weight")
             if isinstance(w, torch.nn.Parameter) and w.dim() >= 2:
-                mod.forward = self._wrap(mod, mod.forward)
+                self._handles.append(mod.register_forward_pre_hook(_fake_quant_pre_hook))
+                self._handles.append(mod.register_forward_hook(_fake_quant_post_hook,
+                                                               always_call=True))
                 self.modules.append(mod)
 
-    @staticmethod
-    def _wrap(mod, forward):
-        def fake_quant_forward(*args, **kwargs):
-            w = mod._parameters["weight"]
-            mod._parameters["weight"] = _StraightThrough.apply(
-                w, fake_quantize_per_channel_symmetric(w))
-            try:
-                return forward(*args, **kwargs)
-            finally:
-                mod._parameters["weight"] = w
-        return fake_quant_forward
-
     def remove(self):
-        for mod in self.modules:
-            del mod.forward  # the instance attribute: the class's forward again
+        for h in self._handles:
+            h.remove()
+        self._handles = []
         self.modules = []
 
 

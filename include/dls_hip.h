@@ -203,6 +203,18 @@ int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nf
                        int64_t ldq, const float *F, int64_t ldf, const float *sz, int64_t sz_row,
                        int64_t sz_chan, const int32_t *rows, const float *weight, int32_t K,
                        float total, float *out, dls_stream_t stream);
+/* The same with a mode (DLS_FEDAVG_EXACT: dls_dequant_fedavg, bit-exact;
+ * DLS_FEDAVG_FMA: the int tiles whose zero points are 0 (symmetric qint8, the
+ * QAT worker's format) accumulate out = fma(q, c, out) with one constant per
+ * (client, channel) c = fl(fl(scale * n_i) / N) — one packed op per element
+ * pair instead of five, a different rounding of each term: within the
+ * north-star's 1e-6 FedAvg tolerance (normwise), not bit-exact; every other
+ * tile runs its exact kernel). */
+int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast,
+                            const void *Q, int64_t ldq, const float *F, int64_t ldf,
+                            const float *sz, int64_t sz_row, int64_t sz_chan, const int32_t *rows,
+                            const float *weight, int32_t K, float total, int32_t mode, float *out,
+                            dls_stream_t stream);
 
 /* Per-segment min / max of x over [seg_off[s], seg_off[s+1]) (torch.aminmax);
  * seg_off is device int64 [nseg+1] with seg_off[nseg] == total.  NaNs are

@@ -93,6 +93,18 @@ def requantize_tensors(flat, layout):
     return q, np.array(scales, np.float32), np.array(zps, np.int32), deq
 
 
+def requantize_model(flat_concat):
+    """The re-quantization at the reference's granularity: ONE quantizer over the
+    concatenated aggregate (``quant(concat_dict_values(aggregated_parameter))``,
+    servers/fed_quant_server.py:39), deterministic MinMax affine 8-bit.
+
+    Returns (q uint8 [n], scale f32, zp int, dequantized f32 [n])."""
+    x = np.asarray(flat_concat, np.float32)
+    s, z = minmax_qparams(np.nanmin(x), np.nanmax(x))
+    q = quantize_affine(x, s, z)
+    return q.astype(np.uint8), s, z, dequant_affine(q, s, z)
+
+
 def dequant_torch_cpu(client_parameter):
     """The reference's own torch op sequence on the CPU
     (servers/fed_quant_server.py:25-33): ``weight.float()`` then a Python loop over

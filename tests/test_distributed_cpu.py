@@ -280,9 +280,12 @@ def _sharded_gtg_worker(rank, world, port, outq):
     dist.destroy_process_group()
 
 
-def test_sharded_gtg_two_ranks_clients_sharded():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gtg_clients_sharded(world):
+    """Each rank receives its own clients into its block of the store; one in-place
+    all-gather fills the other blocks and the rows are adopted without a copy."""
     case = next(c for c in G.shapley_cases() if c["tag"] == "gtg_6_3")
-    out = _spawn(_sharded_gtg_worker)
+    out = _spawn(_sharded_gtg_worker, world)
     for _, sv, _n in out:
         for k, v in case["sv"].items():
             assert abs(sv[int(k)] - v) <= 1e-12

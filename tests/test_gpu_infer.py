@@ -154,3 +154,33 @@ def test_resnet18_fused_eval_matches_torch(deterministic_convs):
         pred = torch.cat([model(xb[i:i + 256]).argmax(1) for i in range(0, xb.shape[0], 256)])
     assert acc0 == int((pred.cpu() == y).sum()) / y.numel()  # the Inferencer's int / n
     assert np.isfinite(float(loss))
+
+
+def test_utility_is_a_function_of_the_model():
+    """the product's default tester (no fixture, default flags)
+    gives bit-identical logits and the same accuracy / loss for the same model on
+    repeated evaluations and on fresh Inferencers, at ResNet-18 x 10k CIFAR-shaped
+    images (the config-5 utility), and leaves torch's global flags as it found them."""
+    from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    torch.manual_seed(7)
+    model = ResNet18().to(dev)
+    X, y = synthetic_classification(10000, (3, 32, 32), seed=11)
+    flags = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    a = Inferencer(model, (X, y), device=dev)
+    assert a.deterministic and a.fused_eval
+    la = a.logits()
+    la2 = a.logits()
+    loss_a, acc_a, _ = a.inference()
+    assert (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark) == flags
+    b = Inferencer(model, (X, y), device=dev)
+    lb = b.logits()
+    loss_b, acc_b, _ = b.inference()
+    assert a._fused_checked is True  # the fused pass matched bn(x) on this stack
+    assert torch.equal(la.view(torch.int32), la2.view(torch.int32))
+    assert torch.equal(la.view(torch.int32), lb.view(torch.int32))
+    assert acc_a == acc_b and float(loss_a) == float(loss_b)
+    assert acc_a == int((la.argmax(1).cpu() == y).sum()) / y.numel()
+    # the module's own forward under the same flags: the same bits
+    plain = Inferencer(model, (X, y), device=dev, fused_eval=False)
+    assert torch.equal(plain.logits().view(torch.int32), la.view(torch.int32))

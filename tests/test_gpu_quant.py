@@ -66,11 +66,13 @@ def test_dequant_fedavg_golden_bit_exact():
     assert same_bits(flat(store.layout.views(out), case["layout"]), z["agg"])
 
 
-def test_fed_quant_server_round_golden():
+@pytest.mark.parametrize("granularity", ["model", "tensor"])
+def test_fed_quant_server_round_golden(granularity):
     from distributed_learning_simulator_amd.servers.fed_quant_server import FedQuantServer
     z, case, payloads = golden_payloads()
     K = case["K"]
-    server = FedQuantServer(tester=None, worker_number=K, synchronous=True)
+    server = FedQuantServer(tester=None, worker_number=K, synchronous=True,
+                            granularity=granularity)
     for i, p in enumerate(payloads):
         server.worker_data_queue.add_task((i, int(z["n"][i]), p))
     for w in range(K):
@@ -79,8 +81,55 @@ def test_fed_quant_server_round_golden():
     # the broadcast model is the re-quantized aggregate (this build's contract, D4)
     res = server.worker_data_queue.get_result(consumer=0)
     agg = z["agg"]
-    q, sc, zp, deq = oquant.requantize_tensors(agg, case["layout"])
+    if granularity == "tensor":
+        q, sc, zp, deq = oquant.requantize_tensors(agg, case["layout"])
+    else:  # one quantizer over concat_dict_values (ref servers/fed_quant_server.py:39)
+        q, sc, zp, deq = oquant.requantize_model(agg)
+        qg, scg, zpg = server.quantized_parameter
+        assert np.array_equal(qg.cpu().numpy(), q)
+        assert float(scg) == float(sc) and int(zpg) == zp
     assert same_bits(flat(res, case["layout"]), deq)
+
+
+def test_fed_quant_model_granularity_resnet18_vs_torch_quantize_per_tensor():
+    """the default re-quantization is the reference's one
+    quantizer over the concatenated aggregate (servers/fed_quant_server.py:37-39).
+    A full ResNet-18 round (2 int8 clients): the one-segment (scale, zero point)
+    equal torch.ao's MinMaxObserver on the concatenated aggregate and the wire
+    bytes equal torch.quantize_per_tensor's int_repr, in concat_dict_values order."""
+    from distributed_learning_simulator_amd.model_shapes import resnet18_cifar
+    from distributed_learning_simulator_amd.servers.fed_quant_server import FedQuantServer
+    g = torch.Generator().manual_seed(44)
+    payloads = []
+    for k in range(2):
+        p = {}
+        for name, s in resnet18_cifar():
+            if len(s) >= 2:
+                p[name] = (torch.randint(-128, 128, s, generator=g, dtype=torch.int8),
+                           torch.rand(s[0], generator=g, dtype=torch.float64) * 1e-3 + 1e-5,
+                           torch.zeros(s[0], dtype=torch.int64))
+            else:
+                p[name] = torch.randn(s, generator=g) * 0.3
+        payloads.append(p)
+    server = FedQuantServer(tester=None, worker_number=2, synchronous=True)
+    assert server.granularity == "model"
+    for i, p in enumerate(payloads):
+        server.worker_data_queue.add_task((i, 100 + 7 * i, p))
+    for w in range(2):
+        server.worker_data_queue.get_result(consumer=w)
+    res = server.worker_data_queue.get_result(consumer=0)
+    concat = torch.cat([v.reshape(-1) for v in server.last_aggregate.values()]).cpu()
+    obs = torch.ao.quantization.MinMaxObserver(dtype=torch.quint8)
+    obs(concat)
+    sc_ref, zp_ref = obs.calculate_qparams()
+    q, sc, zp = server.quantized_parameter
+    assert q.numel() == concat.numel() and sc.numel() == 1 and zp.numel() == 1
+    assert float(sc) == float(sc_ref) and int(zp) == int(zp_ref)
+    qt = torch.quantize_per_tensor(concat, float(sc_ref), int(zp_ref), torch.quint8)
+    assert torch.equal(q.cpu(), qt.int_repr())
+    # the broadcast is the dequantized payload, tensor by tensor
+    deq = torch.cat([v.reshape(-1) for v in res.values()]).cpu()
+    assert torch.equal(deq, (qt.int_repr().float() - int(zp_ref)) * float(sc_ref))
 
 
 @pytest.mark.parametrize("row_len", [1, 3, 15, 16, 17, 27, 576, 4099])
@@ -345,9 +394,20 @@ def test_dequant_fedavg_full_resnet18_k1000_sampled_channels():
             extra[name] = (c,)
     n = torch.randint(100, 1001, (K,), generator=gc).tolist()
     order = torch.randperm(K, generator=gc).tolist()
-    out = st.layout.views(st.fedavg(order, [n[r] for r in order]))
+    exact = st.fedavg(order, [n[r] for r in order])
+    out = st.layout.views(exact)
     torch.cuda.synchronize()
     _check_sampled_channels(st, shapes, out, n, order, gc, extra)
+    # the FMA mode (dls_dequant_fedavg_mode, DLS_FEDAVG_FMA) on the same 1000
+    # clients: within the north-star FedAvg tolerance of the bit-exact aggregate
+    # (normwise 1e-6), every tensor (the IEEE-fallback channel included)
+    from distributed_learning_simulator_amd import _native
+    fma = st.fedavg(order, [n[r] for r in order], mode=_native.FEDAVG_FMA)
+    for name, v in st.layout.views(fma).items():
+        e = out[name].double()
+        err = float((v.double() - e).norm() / e.norm())
+        assert err <= 1e-6, (name, err)
+    assert not torch.equal(fma.view(torch.int32), exact.view(torch.int32))  # a different rounding
 
 
 def test_dequant_fedavg_full_vgg16_sampled_channels():
@@ -459,16 +519,32 @@ def test_dequant_fedavg_lane_tiles_resnet_shapes(K):
         store.write(r, p)
         rows.append(r)
     order = list(torch.randperm(K, generator=g).tolist())
-    full = torch.full((store.layout.P,), float("nan"), device=dev)
-    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order],
-                                          out=full))
-    assert_padding_zero(store.layout, full)
     layout = [(k, tuple(v[0].shape) if isinstance(v, tuple) else tuple(v.shape))
               for k, v in payloads[0].items()]
     clients = [{k: (tuple(t.numpy() for t in v) if isinstance(v, tuple) else v.numpy())
                 for k, v in p.items()} for p in payloads]
     ref = oquant.dequant_fedavg(clients, n, order, layout)
-    assert same_bits(flat(out, layout), ref)
+    from distributed_learning_simulator_amd import _native
+    for mode in (_native.FEDAVG_EXACT, _native.FEDAVG_FMA):
+        full = torch.full((store.layout.P,), float("nan"), device=dev)
+        out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order],
+                                              out=full, mode=mode))
+        assert_padding_zero(store.layout, full)
+        if mode == _native.FEDAVG_EXACT:
+            assert same_bits(flat(out, layout), ref)
+            continue
+        # FMA mode: int8 zero-point-0 tensors take one constant per (client,
+        # channel); the uint8 tensor with zero points and the fp32 biases stay exact
+        off = 0
+        for name, shape in layout:
+            m = int(np.prod(shape))
+            got, want = out[name].reshape(-1).cpu().numpy(), ref[off:off + m]
+            off += m
+            if name == "l2" or name.endswith(".bias"):
+                assert same_bits(got, want), name
+            else:
+                err = np.linalg.norm(got.astype(np.float64) - want) / np.linalg.norm(want)
+                assert err <= 1e-6, (name, err)
 
 
 def test_qat_weight_fake_quant_ste():
@@ -515,6 +591,21 @@ def test_qat_weight_fake_quant_ste():
     names = dict(model.named_parameters())
     assert names["0.weight"] is conv.weight and names["3.weight"] is lin.weight
     assert all(isinstance(p, torch.nn.Parameter) and p.is_leaf for p in names.values())
+    # a deep copy (Trainer.get_inferencer(copy_model=True)) fake-quantizes ITS own
+    # weights, and the hooked model pickles
+    import copy
+    import pickle
+    twin = copy.deepcopy(model)
+    with torch.no_grad():
+        twin[0].weight.mul_(2.0)
+        cw2 = fake_quantize_per_channel_symmetric(twin[0].weight)
+        y3 = twin(x)
+        ref3 = F.linear(F.relu(F.conv2d(x, cw2, twin[0].bias)).flatten(1),
+                        fake_quantize_per_channel_symmetric(twin[3].weight), twin[3].bias)
+    assert torch.allclose(y3, ref3, rtol=0, atol=1e-5)
+    assert twin[0].weight is dict(twin.named_parameters())["0.weight"]
+    assert len(pickle.dumps(model.cpu())) > 0
+    model.to(dev)
     hooks.remove()
     plain = F.linear(F.relu(F.conv2d(x, conv.weight, conv.bias)).flatten(1), lin.weight, lin.bias)
     assert torch.allclose(model(x), plain, rtol=0, atol=1e-6)

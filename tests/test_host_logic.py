@@ -372,3 +372,31 @@ def test_data_serialization_size_matches_pickle():
     for data in (params, q, (torch.zeros(100, dtype=torch.uint8), torch.ones(3), torch.zeros(3, dtype=torch.int32))):
         assert get_data_serialization_size(data) == len(pickle.dumps(data))
     assert get_data_serialization_size(q) < get_data_serialization_size(params)
+
+
+def test_sliced_store_write_views_row():
+    """SlicedClientUpdateStore (the bit-exact sharded exchange's slice-major rows):
+    a dict written tensor by tensor across slice boundaries reads back exactly,
+    as views / copies and as a flat row; block B[d] is slice d of every row."""
+    from distributed_learning_simulator_amd.aggregation import SlicedClientUpdateStore
+    from distributed_learning_simulator_amd.distributed import slice_bounds
+    from distributed_learning_simulator_amd.layout import ParameterLayout
+    shapes = [("a", (3, 50)), ("b", (7,)), ("c", (4, 4, 9)), ("d", (130,))]
+    layout = ParameterLayout(shapes)
+    for world in (1, 2, 3, 5):
+        L = slice_bounds(layout.P, world)[1]
+        st = SlicedClientUpdateStore(layout, "cpu", 1, world, L)
+        g = torch.Generator().manual_seed(world)
+        ds = [{n: torch.randn(s, generator=g) for n, s in shapes} for _ in range(3)]
+        rows = [st.acquire() for _ in ds]  # grows past capacity 1
+        for r, d in zip(rows, ds):
+            st.write(r, d)
+        for r, d in zip(rows, ds):
+            v = st.views(r)
+            flat = layout.flatten(d)
+            assert torch.equal(st.row(r), flat)
+            for n, _ in shapes:
+                assert torch.equal(v[n], d[n])
+            for s_ in range(world):
+                assert torch.equal(st.B[s_, r], torch.cat([flat, torch.zeros(world * L - layout.P)])
+                                   [s_ * L:(s_ + 1) * L])
