@@ -679,14 +679,17 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     (batched bit-exact subset models + ResNet-18 test-set inference; on N ranks the
     coalitions are dealt round-robin and the utilities all-reduced).  Weak scaling:
     args.evals coalitions per GPU.  Timed with the tester's default GPU forward (the
-    value: every eval batch norm + residual + ReLU one hand-written pass, logits
-    bit-identical to the module's forward) and again with the module's own forward
-    (``fused_eval=False``: MIOpen batch norm, separate add and ReLU kernels)."""
+    value: deterministic convolution algorithms, so a coalition's utility is a
+    function of the coalition; every eval batch norm + residual + ReLU one
+    hand-written pass, logits bit-identical to the module's forward), again with the
+    module's own forward (``fused_eval=False``: MIOpen batch norm, separate add and
+    ReLU kernels), and with non-deterministic convolutions (the cost of determinism)."""
     server = _shapley_eval_server(args, dev)
     coal = _shapley_coalitions(50, (args.evals + 2) * world, SEED + 7)
 
-    def timed(fused):
+    def timed(fused, deterministic=True):
         server.tester.fused_eval = fused
+        server.tester.deterministic = deterministic
         server.evaluate_subsets(coal[: 2 * world])  # MIOpen kernel selection, warm caches
         torch.cuda.synchronize()
         if world > 1:
@@ -701,6 +704,10 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
 
     el, vals = timed(True)
     el_m, vals_m = timed(False)
+    # the cost of reproducible utilities: the same path with MIOpen free to pick
+    # non-deterministic convolution algorithms (not the product's default)
+    el_nd, _ = timed(True, deterministic=False)
+    server.tester.deterministic = True
     n = len(coal) - 2 * world
     del server
     torch.cuda.empty_cache()
@@ -711,6 +718,12 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
             "value": round(n / el, 3), "unit": "subset-evals/s (all GPUs)",
             "ms_per_eval_per_gpu": round(el / n * world * 1e3, 2),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
+            "deterministic_convs": True,
+            "nondeterministic_convs": {"value": round(n / el_nd, 3),
+                                       "unit": "subset-evals/s (all GPUs)",
+                                       "note": "the same path with MIOpen's default (not "
+                                               "run-to-run reproducible) convolution algorithms: "
+                                               "what determinism costs"},
             "module_forward": {"value": round(n / el_m, 3), "unit": "subset-evals/s (all GPUs)",
                                "ms_per_eval_per_gpu": round(el_m / n * world * 1e3, 2),
                                "max_utility_diff": round(

@@ -261,6 +261,10 @@ struct UnionDiv {
 __device__ __forceinline__ f32x4 addu(f32x4 a, f32x4 b) { return a + b; }
 constexpr int kUnionWaves = 16;
 constexpr int kUnionKMax = 8;   // coalitions per wave (the plan caps it; 16 x 8 >= 64)
+#ifndef DLS_UNION_AHEAD
+#define DLS_UNION_AHEAD 2
+#endif
+constexpr int kUnionAhead = DLS_UNION_AHEAD;  // tiles of client rows in flight (1 or 2)
 
 template <bool ACC>
 __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
@@ -317,9 +321,11 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             load[bw] += lens[best] + 2;  // + the coalition's fixed cost
         }
     }
-    // loader slots: wave wv stages clients wv + W l (l < NL) that exist
-    f32x4 R[NL];
-    auto issue = [&](int64_t t) {
+    // loader slots: wave wv stages clients wv + W l (l < NL) that exist; two
+    // register sets, so that the loads of the next TWO tiles are in flight while a
+    // tile is computed (kUnionAhead = 2; the LDS holds only two staged tiles)
+    f32x4 RA[NL], RB[NL];
+    auto issue = [&](int64_t t, f32x4 (&R)[NL]) {
         const int64_t i0 = t * 64 + lane;
         const int64_t iq = i0 < P4 ? i0 : P4 - 1;
 #pragma unroll
@@ -331,7 +337,7 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             }
         }
     };
-    auto stage = [&](int b) {  // t_j = fl(x_j * n_j) into buffer b; out-of-range flag
+    auto stage = [&](int b, const f32x4 (&R)[NL]) {  // t_j = fl(x_j * n_j) into buffer b; out-of-range flag
         uint32_t bad = 0;
 #pragma unroll
         for (int l = 0; l < NL; ++l) {
@@ -349,8 +355,12 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
         }
         if (lane == 0) tbad[b][wv] = bad;
     };
-    issue(tile);
-    stage(0);
+    issue(tile, RA);
+    stage(0, RA);
+    if (kUnionAhead > 1) {
+        if (tile + gridDim.x < ntiles) issue(tile + gridDim.x, RA);
+        if (tile + 2 * (int64_t)gridDim.x < ntiles) issue(tile + 2 * (int64_t)gridDim.x, RB);
+    }
     __syncthreads();  // buffer 0 and the plan are ready
     const int nk = __builtin_amdgcn_readfirstlane(plan[wv][0]);
     int cid[kUnionKMax];
@@ -361,7 +371,9 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
     for (int k = 0; k < kUnionKMax; ++k)
         if (k < nk) fast &= (int)((__float_as_uint(cst[cid[k]].w) & 2u) != 0);
     int b = 0;
-    for (; tile < ntiles; tile += gridDim.x, b ^= 1) {
+    // one tile: Rs holds the loads of the next tile (staged after the compute),
+    // then takes those of the tile after the one in flight in the other set
+    auto one_tile = [&](f32x4 (&Rs)[NL]) {
         const int64_t i0 = tile * 64 + lane;
         const int64_t iq = i0 < P4 ? i0 : P4 - 1;
         const int64_t next = tile + gridDim.x;
@@ -369,7 +381,7 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
 #pragma unroll
         for (int k = 0; k < kUnionKMax; ++k)
             if (ACC && k < nk) res[k] = out[(int64_t)cid[k] * ldo4 + iq];
-        if (next < ntiles) issue(next);  // in flight during this tile's coalitions
+        if (kUnionAhead == 1 && next < ntiles) issue(next, Rs);  // in flight during this tile's coalitions
         uint32_t anybad = 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) anybad |= tbad[b][w];
@@ -468,12 +480,29 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             }
             res[k] = acc;
         }
-        if (next < ntiles) stage(b ^ 1);  // the next tile's t (its loads have landed by now)
+        if (next < ntiles) stage(b ^ 1, Rs);  // the next tile's t (its loads have landed by now)
+        if (kUnionAhead > 1 && next + 2 * (int64_t)gridDim.x < ntiles)
+            issue(next + 2 * (int64_t)gridDim.x, Rs);
 #pragma unroll
         for (int k = 0; k < kUnionKMax; ++k)
             if (k < nk && i0 < P4)
                 out[(int64_t)cid[k] * ldo4 + i0] = res[k];
         __syncthreads();  // buffer b ^ 1 is complete; buffer b free for the tile after next
+    };
+    if (kUnionAhead == 1) {
+        for (; tile < ntiles; tile += gridDim.x, b ^= 1) one_tile(RA);
+    } else {
+        // the register sets alternate (a copy of an in-flight load's registers
+        // would wait for it), so the loop is unrolled by two
+        while (tile < ntiles) {
+            one_tile(RA);
+            tile += gridDim.x;
+            b ^= 1;
+            if (tile >= ntiles) break;
+            one_tile(RB);
+            tile += gridDim.x;
+            b ^= 1;
+        }
     }
 }
 

@@ -725,9 +725,9 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         for (int c = 0; c < kSpanMax; ++c)
             v[c] = sz[(int64_t)min(wt.t.chan0 + c, wt.t.chan_end - 1) * L.chan + (int64_t)r * L.row];
     };
-    struct One {
-        u32x4 qv[G];
-        f32x2 s[G];
+    struct One1 {
+        u32x4 qv;
+        f32x2 s;
         float wk;
     };
     struct SOne {
@@ -735,8 +735,11 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         float wk;
         int j;
     };
+    // clients per batch: kLaneUS on 1 KiB tiles, 1 on wider ones (G KiB per
+    // client already; two batches in flight per wave either way)
+    constexpr int US = G > 1 ? 1 : kLaneUS;
     struct SBatch {
-        SOne c[kLaneUS];
+        SOne c[US];
     };
     ChunkRows cr;
     cr.init(rows, w, K);
@@ -801,15 +804,15 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
                     }
                 }
             };
-            chunk_pipeline_1tail<kLaneUS, SBatch>(
+            chunk_pipeline_1tail<US, SBatch>(
                 n,
                 [&](int j0, SBatch &b) {
 #pragma unroll
-                    for (int u = 0; u < kLaneUS; ++u) sfetch(j0 + u, b.c[u]);
+                    for (int u = 0; u < US; ++u) sfetch(j0 + u, b.c[u]);
                 },
                 [&](const SBatch &b) {
 #pragma unroll
-                    for (int u = 0; u < kLaneUS; ++u) sstep(b.c[u]);
+                    for (int u = 0; u < US; ++u) sstep(b.c[u]);
                 },
                 [&](int j) {
                     SOne b;
@@ -818,48 +821,43 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
                 });
             continue;
         }
-        auto fetch = [&](int j, One &b) {
-            const int64_t r = readlane_i(tr, j);
-            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
-                b.s[g] = sz[coff[g] + r * L.row];
-            }
-            b.wk = readlane_f(tw, j);
+        // per-client path (chunks that fail the check, tiles over more than
+        // kSpanMax channels): the lane's (scale, zero point) gathered with each
+        // client's payload, one wave-uniform decision per client (exact fl(zp * s)
+        // and the fast division range on every lane).  One KiB slice at a time, so
+        // that this path's registers stay within the staged path's.
+        auto rare = [&](auto g_c) {
+            constexpr int g = decltype(g_c)::value;
+            auto fetch = [&](int j, One1 &b) {
+                const int64_t r = readlane_i(tr, j);
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+                b.qv = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+                b.s = sz[coff[g] + r * L.row];
+                b.wk = readlane_f(tw, j);
+            };
+            auto step = [&](const One1 &b) {
+                const float zs = b.s.y * b.s.x;
+                const int ok = d.fast & (int)(__builtin_fmaf(b.s.y, b.s.x, -zs) == 0.f) &
+                               (int)scale_fast(b.s.x * b.wk);
+                if (__builtin_expect(__ballot(!ok) == 0, 1))
+                    accum16_one<true, true, SIGNED, TWO, kLaneSched>(acc[g], b.qv, b.s.x, zs, 0.f,
+                                                                     b.wk, d);
+                else  // rare clients: the reference's formula with IEEE division
+                    accum16_one<false, false, SIGNED>(acc[g], b.qv, b.s.x, 0.f, b.s.y, b.wk, d);
+            };
+            chunk_pipeline<1, One1>(
+                n, [&](int j0, One1 &bb) { fetch(j0, bb); }, [&](const One1 &bb) { step(bb); },
+                [&](int j) {
+                    One1 bb;
+                    fetch(j, bb);
+                    step(bb);
+                });
         };
-        auto step = [&](const One &b) {
-            // one wave-uniform decision per client: exact fl(zp * s) and the fast
-            // division range on every lane and slice (always, for symmetric int8)
-            int ok = d.fast;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float zs = b.s[g].y * b.s[g].x;
-                ok &= (int)(__builtin_fmaf(b.s[g].y, b.s[g].x, -zs) == 0.f) &
-                      (int)scale_fast(b.s[g].x * b.wk);
-            }
-            if (__builtin_expect(__ballot(!ok) == 0, 1)) {
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    accum16_one<true, true, SIGNED, TWO, kLaneSched>(
-                        acc[g], b.qv[g], b.s[g].x, b.s[g].y * b.s[g].x, 0.f, b.wk, d);
-            } else {  // rare clients: the reference's formula with IEEE division
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    accum16_one<false, false, SIGNED>(acc[g], b.qv[g], b.s[g].x, 0.f, b.s[g].y,
-                                                      b.wk, d);
-            }
-        };
-        // one client per batch, double-buffered: these registers stay within the
-        // staged path's
-        chunk_pipeline<1, One>(
-            n, [&](int j0, One &b) { fetch(j0, b); }, [&](const One &b) { step(b); },
-            [&](int j) {
-                One b;
-                fetch(j, b);
-                step(b);
-            });
+        rare(std::integral_constant<int, 0>{});
+        if constexpr (G > 1) rare(std::integral_constant<int, 1>{});
+        if constexpr (G > 2) rare(std::integral_constant<int, 2>{});
+        if constexpr (G > 3) rare(std::integral_constant<int, 3>{});
     }
     store_tile<G>(wt, acc, out);
 }
@@ -1342,12 +1340,6 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
     }
     DLS_REQUIRE(ntiles > 0 && K > 0 && nf <= ntiles, DLS_EINVAL,
                 "dls_dequant_fedavg: ntiles=%d grouped tiles=%lld K=%d", ntiles, (long long)nf, K);
-    // multi-channel tiles are cut at 1 KiB (the wider lane kernels measured no
-    // faster and are not built): groups 4-6 stay in the numbering, empty
-    DLS_REQUIRE(nfast[4] == 0 && nfast[5] == 0 && nfast[6] == 0, DLS_EINVAL,
-                "dls_dequant_fedavg: multi-channel int tiles of 4/3/2 KiB (nfast[4..6] = %d, %d, "
-                "%d) are not supported; cut them into 1 KiB tiles (group 7)",
-                nfast[4], nfast[5], nfast[6]);
     DLS_REQUIRE(ldq % 16 == 0 && ldf % 4 == 0 && aligned16(out) && (!Q || aligned16(Q)) &&
                     (!F || aligned16(F)),
                 DLS_ELAYOUT, "dls_dequant_fedavg: ldq %% 16, ldf %% 4, 16-byte alignment");
@@ -1360,8 +1352,8 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
     const SzLayout L{sz_row, sz_chan};
     hipStream_t st = as_stream(stream);
     constexpr int wpb = kBlock / 64;
-    // Groups: 0-3 one-channel tiles of 4/3/2/1 KiB slices, 7 lane-channel tiles
-    // of 1 KiB (4-6 empty), 8 fp32 tiles, 9 small int tiles, then the general tiles.  The group with
+    // Groups: 0-3 one-channel tiles of 4/3/2/1 KiB slices, 4-7 lane-channel tiles
+    // of 4/3/2/1 KiB, 8 fp32 tiles, 9 small int tiles, then the general tiles.  The group with
     // the most bytes runs on the caller's stream; every other non-empty group on a
     // side stream of its own, concurrently (their waves walk all K clients, so a
     // small group is a long latency chain, not a small amount of work), and the
@@ -1411,9 +1403,12 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
          k_dequant_fast<2, false, true>},
         {k_dequant_fast<1, false, false>, k_dequant_fast<1, true, false>,
          k_dequant_fast<1, false, true>},
-        {nullptr, nullptr, nullptr},  // groups 4-6: rejected above
-        {nullptr, nullptr, nullptr},
-        {nullptr, nullptr, nullptr},
+        {k_dequant_lanes<4, false, false>, k_dequant_lanes<4, true, false>,
+         k_dequant_lanes<4, false, true>},
+        {k_dequant_lanes<3, false, false>, k_dequant_lanes<3, true, false>,
+         k_dequant_lanes<3, false, true>},
+        {k_dequant_lanes<2, false, false>, k_dequant_lanes<2, true, false>,
+         k_dequant_lanes<2, false, true>},
         {k_dequant_lanes<1, false, false>, k_dequant_lanes<1, true, false>,
          k_dequant_lanes<1, false, true>}};
     // A wave walks all K clients, so waves are long and equal: a group is launched

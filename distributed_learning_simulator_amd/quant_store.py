@@ -28,8 +28,11 @@ from .layout import ALIGN, ParameterLayout, _round_up
 
 TILE = 1024  # one wavefront slice: 64 lanes x 16 elements
 FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
-LANE_TILE = TILE  # multi-channel tiles (channel rows a multiple of 16): one slice per wavefront
-# (dls_dequant_fedavg rejects wider ones: their kernels measured no faster)
+# multi-channel tiles (channel rows a multiple of 16): "adaptive" = the widest of
+# 4 / 2 / 1 KiB that spans at most 3 channel rows (4 KiB for rows >= 2048, 2 KiB
+# for rows >= 1024: every lane's channel constants stay in the kernel's staged
+# table), or a fixed width in elements
+LANE_TILE = "adaptive"
 F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
 FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
 QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
@@ -108,10 +111,12 @@ class QuantLayout:
           channel rows are long (>= 1024, multiple of 64) and fill 1 KiB slices
           well get channel-aligned tiles of up to FAST_TILE elements (a wave
           streams up to 4 KiB of every client row with one (scale, zp) per client);
-        * lane-channel tiles (group 7; groups 4-6, wider ones, stay empty): the
-          other int tensors whose channel rows are a multiple of 16 elements (no
-          lane's 16-element chunk straddles two channels: 3x3 convs, fc layers) are
-          cut into 1 KiB tiles from their start, each lane in its own channel;
+        * lane-channel tiles (groups 4-7: 4, 3, 2, 1 KiB slices): the other int
+          tensors whose channel rows are a multiple of 16 elements (no lane's
+          16-element chunk straddles two channels: 3x3 convs, fc layers) are cut
+          into LANE_TILE-element tiles from their start, each lane in its own
+          channel (adaptive: 4 KiB tiles for rows >= 2048, 2 KiB for rows >= 1024,
+          else 1 KiB: at most 3 channels per tile);
         * fp32 tiles (group 8, <= F32_TILE elements): the fp32 tensors;
         * small int tiles (group 9, <= F32_TILE elements): the other int tensors
           with rows of at least 4 elements (a lane's 4 span <= 2 channels), except
@@ -133,8 +138,11 @@ class QuantLayout:
                                      j, cend))
                 continue
             if kind and rl % 16 == 0:
-                for e in range(0, n, LANE_TILE):
-                    lane_rows.append((off + e, src + e, min(LANE_TILE, n - e), kind, cb + e // rl,
+                lt = LANE_TILE
+                if lt == "adaptive":
+                    lt = 4096 if rl >= 2048 else (2048 if rl >= 1024 else TILE)
+                for e in range(0, n, lt):
+                    lane_rows.append((off + e, src + e, min(lt, n - e), kind, cb + e // rl,
                                       rl, e % rl, cend))
                 continue
             if not kind:

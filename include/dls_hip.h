@@ -191,10 +191,10 @@ typedef struct dls_qtile {
  * r * sz_row + c * sz_chan (the store keeps them channel-major: sz_row = 1).
  * nfast: host array of DLS_QTILE_GROUPS counts; the table starts with
  * nfast[0..3] one-channel int tiles of 4, 3, 2, 1 KiB slices (every real
- * element in channel chan0), then nfast[7] multi-channel int tiles of 1 KiB
- * (channel rows a multiple of 16 elements: no lane's 16-element chunk straddles
- * two channels; nfast[4..6], wider multi-channel tiles, must be 0, else
- * DLS_EINVAL), then nfast[8] fp32 tiles of <= 256 elements,
+ * element in channel chan0), then nfast[4..7] multi-channel int tiles of 4, 3,
+ * 2, 1 KiB slices (channel rows a multiple of 16 elements: no lane's 16-element
+ * chunk straddles two channels; a tile spanning more than 4 channels takes the
+ * per-client path), then nfast[8] fp32 tiles of <= 256 elements,
  * nfast[9] int tiles of <= 256 elements of tensors with channel rows of >= 4
  * elements (a lane's 4 elements span at most two channels); the remaining tiles
  * (len <= 1024) are int tiles of any shape (see dls_qtile). */

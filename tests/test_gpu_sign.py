@@ -268,3 +268,33 @@ def test_vote_signs_packed_1000_clients_resnet18_every_parameter():
     S = pos - neg
     S[(pos == 1) & (neg == 1)] = np.nan  # the NaN code
     assert same_bits(sign[idx].cpu().numpy(), osign.majority_vote(S))
+
+
+@pytest.mark.parametrize("P", [5_000_004, 14_000_000])
+def test_vote_balanced_wave_ranges(P):
+    """The large-model vote gives every wave a contiguous range of R groups so that
+    the chip gets a whole number of waves per CU (R = ceil(groups / (4 x CUs)):
+    G = ceil(R / 64) = 2 here at P = 5M and 4 at P = 14M, the last 64-group chunk
+    of a range partial, ranges not 64-aligned).  Signs, packed vote and counts
+    (with a row subset) against torch's sum-of-signs on the same ternary matrix."""
+    from distributed_learning_simulator_amd import _native
+    K = 13
+    g = torch.Generator(device=dev).manual_seed(P % 1000)
+    S = torch.randint(-1, 2, (K, P), generator=g, device=dev, dtype=torch.int8).float()
+    Wd = _native.sign_words(P)
+    planes = torch.zeros((K, Wd), dtype=torch.int64, device=dev)
+    _native.sign_pack(S, P, planes)
+    ref = torch.sign(S.sum(0))
+    sign = torch.empty(P, device=dev)
+    vote = torch.full((Wd,), 0x55, dtype=torch.int64, device=dev)
+    _native.sign_vote(planes, None, K, P, sign, vote_planes=vote)
+    assert torch.equal(sign, ref)
+    c = torch.empty(P, dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, None, K, P, c)
+    assert torch.equal(c, S.sum(0).int())
+    v2 = torch.zeros(Wd, dtype=torch.int64, device=dev)
+    _native.sign_from_counts(c, P, None, v2)
+    assert torch.equal(vote, v2)
+    rows = torch.tensor([12, 0, 5, 7, 3], dtype=torch.int32, device=dev)
+    _native.sign_vote_count(planes, rows, len(rows), P, c)
+    assert torch.equal(c, S[rows.long()].sum(0).int())

@@ -50,19 +50,24 @@ def test_abi_version_and_error_without_gpu(lib):
     assert b"null pointer" in lib.dls_last_error()
 
 
-def test_dequant_rejects_wide_lane_tiles_without_gpu(lib):
-    """Multi-channel tiles are 1 KiB (group 7); a table with tiles in groups 4-6
-    fails before any device call (no pointer is dereferenced on the host)."""
-    f = lib.dls_dequant_fedavg
+def test_dequant_rejects_bad_mode_without_gpu(lib):
+    """dls_dequant_fedavg_mode validates its mode (DLS_FEDAVG_EXACT / _FMA) and the
+    tile-group counts before any device call (no pointer is dereferenced on the
+    host)."""
+    f = lib.dls_dequant_fedavg_mode
     f.restype = ctypes.c_int
     dummy = ctypes.c_void_p(16)  # never dereferenced: validation comes first
-    for g in (4, 5, 6):
-        nfast = (ctypes.c_int32 * 10)(*[1 if i == g else 0 for i in range(10)])
+    nfast = (ctypes.c_int32 * 10)(*[0] * 7, 1, 0, 0)
+    for mode, what in ((2, b"mode"), (-1, b"mode")):
         rc = f(dummy, 1, nfast, dummy, ctypes.c_int64(1024), None, ctypes.c_int64(4), dummy,
                ctypes.c_int64(1), ctypes.c_int64(1), dummy, dummy, 1, ctypes.c_float(1.0),
-               dummy, None)
-        assert rc == -1
-        assert b"1 KiB tiles" in lib.dls_last_error()
+               mode, dummy, None)
+        assert rc == -1 and what in lib.dls_last_error()
+    bad = (ctypes.c_int32 * 10)(*[0] * 7, -1, 0, 0)
+    rc = f(dummy, 1, bad, dummy, ctypes.c_int64(1024), None, ctypes.c_int64(4), dummy,
+           ctypes.c_int64(1), ctypes.c_int64(1), dummy, dummy, 1, ctypes.c_float(1.0), 0, dummy,
+           None)
+    assert rc == -1 and b"nfast[7]" in lib.dls_last_error()
 
 
 def test_product_path_has_no_oracle_import():

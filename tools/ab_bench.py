@@ -173,29 +173,25 @@ def setup(dev, want=()):
                      4 * sum(m for m, k in zip(sr.layout.numels, qlr.kinds) if not k) + 8 * qlr.C) \
             + 4 * sr.layout.numel
         saved = qs.LANE_TILE
-        for lt, fwv in ((1, None), (1, 0), (1, 8), (1, 16)):  # lane tiles are 1 KiB
-            qs.LANE_TILE = 1024 * lt
-            fw, qs.FAST_WASTE = qs.FAST_WASTE, (qs.FAST_WASTE if fwv is None else fwv)
-            tt, nft = qlr.tiles()
-            qs.FAST_WASTE = fw
-            tdev = torch.from_numpy(tt.view(np.uint8).copy()).to(dev)
-            W[f"quant_r18_l{lt}" + (f"_w{fwv}" if fwv is not None else "")] = (
-                lambda L, tdev=tdev, tt=tt, nft=nft: L.dls_dequant_fedavg(
-                    ptr(tdev), len(tt), nfast_arg(L, nft), ptr(sr.Q), sr.Q.stride(0), ptr(sr.F),
-                    sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
-                    ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb, qo18)
-        qs.LANE_TILE = saved
-        W["quant_r18"] = W[f"quant_r18_l{saved // 1024}"]
-        tt, nft = qlr.tiles()
-        tdev0 = torch.from_numpy(tt.view(np.uint8).copy()).to(dev)
 
-        def qmode(rows_t, w_t, tot, mode):
+        def table(lane_tile):
+            qs.LANE_TILE = lane_tile
+            tt, nft = qlr.tiles()
+            qs.LANE_TILE = saved
+            return torch.from_numpy(tt.view(np.uint8).copy()).to(dev), tt, nft
+
+        def qmode(tab, rows_t, w_t, tot, mode):
+            tdev, tt, nft = tab
             return lambda L: L.dls_dequant_fedavg_mode(
-                ptr(tdev0), len(tt), nfast_arg(L, nft), ptr(sr.Q), sr.Q.stride(0), ptr(sr.F),
+                ptr(tdev), len(tt), nfast_arg(L, nft), ptr(sr.Q), sr.Q.stride(0), ptr(sr.F),
                 sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
                 ptr(rows_t), ptr(w_t), rows_t.numel(), tot, mode, ptr(qo18), stream())
+        tab_p, tab_1 = table(saved), table(1024)  # the store's default tiling; 1 KiB lane tiles
+        W["quant_r18"] = (qmode(tab_p, r1k, w1k, t1k, 0), nb, qo18)
+        W["quant_r18_l1"] = (qmode(tab_1, r1k, w1k, t1k, 0), nb, qo18)
         # DLS_FEDAVG_FMA (1e-6 tolerance mode) on the same 1000 clients
-        W["quant_r18_fma"] = (qmode(r1k, w1k, t1k, 1), nb, qo18)
+        W["quant_r18_fma"] = (qmode(tab_p, r1k, w1k, t1k, 1), nb, qo18)
+        W["quant_r18_l1_fma"] = (qmode(tab_1, r1k, w1k, t1k, 1), nb, qo18)
         # >= 10 ms dispatches for clock / counter probes: the 1000 client rows walked
         # 5 times (K = 5000, every pass from HBM: 11 GB >> L2 + MALL), and the same
         # arithmetic with every client on row 0 (payload loads L2-resident)
@@ -203,9 +199,10 @@ def setup(dev, want=()):
         w5k = w1k.repeat(5)
         t5k = float(w5k.sum())
         nb5 = 5 * (nb - 4 * sr.layout.numel) + 4 * sr.layout.numel
-        W["quant_r18_k5000"] = (qmode(r5k, w5k, t5k, 0), nb5)
-        W["quant_r18_k5000_fma"] = (qmode(r5k, w5k, t5k, 1), nb5)
-        W["quant_r18_k5000_l2"] = (qmode(torch.zeros_like(r5k), w5k, t5k, 0), nb5)
+        W["quant_r18_k5000"] = (qmode(tab_p, r5k, w5k, t5k, 0), nb5)
+        W["quant_r18_k5000_fma"] = (qmode(tab_p, r5k, w5k, t5k, 1), nb5)
+        W["quant_r18_k5000_l2"] = (qmode(tab_p, torch.zeros_like(r5k), w5k, t5k, 0), nb5)
+        tt, nft = tab_p[1], tab_p[2]
         if "quant_r18_slab" in want:
             # slab-major emulation: every Q tile of <= 1 KiB gets its own slab of
             # 1000 consecutive 1 KiB client pieces (ldq = 1 KiB, src = slab start),

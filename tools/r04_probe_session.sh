@@ -19,6 +19,8 @@ step ab_vote.txt env DLS_VARIANTS="$ROOT/tools/_variants/vote" timeout -k 10 300
     python -u tools/ab_bench.py --workloads vote_sign,vote --check --rounds 7
 step ab_quant.txt env DLS_VARIANTS="$ROOT/tools/_variants/quant" timeout -k 10 400 \
     python -u tools/ab_bench.py --workloads quant_r18,quant_r18_fma,quant_r18_k5000,quant_r18_k5000_fma,quant_r18_k5000_l2 --rounds 5
+step ab_union.txt env DLS_VARIANTS="$ROOT/tools/_variants/union" timeout -k 10 300 \
+    python -u tools/ab_bench.py --workloads union --check --rounds 7
 cd /tmp && export TMPDIR=/tmp
 # the valu probe under the SQ counters (each dispatch its own row)
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
