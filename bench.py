@@ -107,10 +107,16 @@ def load_traffic(key):
 
 
 def valu_issue(kernel, key):
-    """The VALU issue roof from counters: the fraction of the 1024 SIMDs' cycles
-    their VALU was busy while this workload's kernels ran (4 x SQ_ACTIVE_INST_VALU
-    / (1024 x GRBM_GUI_ACTIVE / 8), profiles/pmc_traffic.json); 1.0 = every SIMD
-    issuing a VALU instruction every 4 cycles.  None without the SQ pass."""
+    """The VALU issue roof from counters, for kernels whose VALU stream is fp32
+    arithmetic: the fraction of the 1024 SIMDs' cycles their VALU was busy while
+    this workload's kernels ran, 4 x SQ_INSTS_VALU / (1024 x GRBM_GUI_ACTIVE / 8)
+    (profiles/pmc_traffic.json).  The 4 cycles per wave64 instruction are measured
+    (tools/valu_issue_probe.hip, profiles/r04a_valu_issue.txt): v_fma_f32,
+    v_pk_fma_f32, v_pk_mul_f32 and v_cvt_f32_ubyte issue at 4.0-4.3 SIMD cycles
+    per wave-instruction with the SIMD saturated, but 32-bit integer / logic ops
+    (v_xor_b32, v_add_u32, v_bitop3_b32) at ~2.5, so the formula overstates an
+    integer-heavy kernel (the sign kernels read 1.1 in round 3) and is not
+    reported for them.  None without the SQ pass."""
     f = load_pmc(key).get("valu_busy_frac")
     if f is None:
         return None
@@ -308,7 +314,6 @@ def bench_sign(args, dev):
         "ms_per_step": round(ms, 4),
         "roofline": roofline("dls_sign_vote", bytes_per_launch, kms, key="sign_vote"),
         "pack": roofline("dls_sign_pack_f32", 16 * (P * 4 + W * 8), pkms, key="sign_pack"),
-        "valu_issue": valu_issue("dls_sign_vote", "sign_vote"),
     }
 
 
@@ -420,8 +425,9 @@ def bench_quant(args, dev, K=100, shapes=None, model="VGG-16", key="fed_quant"):
         def step(a=None, b=None):
             if a is not None:
                 a.record()
-            _native.dequant_fedavg(store.tiles, store.ntiles, store.nfast, store.Q, store.F,
-                                   store.sz, rows_t, w_t, total, out, mode=mode)
+            tiles, ntiles, nfast = store.table(mode)
+            _native.dequant_fedavg(tiles, ntiles, nfast, store.Q, store.F, store.sz, rows_t, w_t,
+                                   total, out, mode=mode)
             if b is not None:
                 b.record()
         return step

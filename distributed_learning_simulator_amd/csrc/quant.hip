@@ -23,6 +23,10 @@ constexpr int kQuantSched = 2;  // element pairs between scheduling barriers
 #define DLS_LANE_US 2
 #endif
 constexpr int kLaneUS = DLS_LANE_US;  // clients per batch on lane-channel tiles (staged path)
+#ifndef DLS_LANE_USG
+#define DLS_LANE_USG 1
+#endif
+constexpr int kLaneUSG = DLS_LANE_USG;  // the same on multi-KiB lane tiles
 #ifndef DLS_LANE_SCHED
 #define DLS_LANE_SCHED 2
 #endif
@@ -735,9 +739,9 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         float wk;
         int j;
     };
-    // clients per batch: kLaneUS on 1 KiB tiles, 1 on wider ones (G KiB per
-    // client already; two batches in flight per wave either way)
-    constexpr int US = G > 1 ? 1 : kLaneUS;
+    // clients per batch: kLaneUS on 1 KiB tiles, kLaneUSG on wider ones (G KiB
+    // per client already; two batches in flight per wave either way)
+    constexpr int US = G > 1 ? kLaneUSG : kLaneUS;
     struct SBatch {
         SOne c[US];
     };

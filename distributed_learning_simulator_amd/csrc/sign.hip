@@ -132,15 +132,15 @@ struct HSCounter {
     }
 };
 
-// Vote kernel: wave w owns the contiguous range of R groups (64 parameters
-// each) [w R, (w+1) R); lane l owns groups w R + l + 64 q, q < G = ceil(R/64),
+// Vote kernel: wave w of nw owns the contiguous range of groups (64 parameters
+// each) [w VG / nw, (w+1) VG / nw) (VG = vote groups; sizes differ by at most
+// one); lane l owns groups wlo + l + 64 q, q < G = ceil(range / 64),
 // and walks all K clients: one 16-byte [pos, neg] load per client and group,
 // batches of 8 clients through the carry-save counters.  The grid is one
 // generation of resident waves sweeping the client rows in step.  On large
-// models R is chosen so that the chip gets a whole number of waves per CU
-// (kVoteWPC x CUs): every CU then streams the same number of bytes — with
-// R = 256 (682 waves on ResNet-18) a third of the CUs held 3 waves and the rest
-// 2, and the CUs with 3 set the time.  Epilogue: the counters are already
+// models nw = kVoteWPC x CUs, a whole number of waves per CU: every CU then
+// streams the same number of bytes — with 256 groups per wave (682 waves on
+// ResNet-18) a third of the CUs held 3 waves and the rest 2.  Epilogue: the counters are already
 // bit-sliced (bit b of parameter j's count = bit j of word b), so the fp32 sign
 // needs no unpacking: a bit-sliced comparison of the pos / neg counters gives
 // two words (gt, lt) per group.  Those words (or, when the int32 counts are
@@ -154,7 +154,7 @@ constexpr int kVoteWPBMax = 4;  // waves per block
 #ifndef DLS_VOTE_WPB
 #define DLS_VOTE_WPB 4
 #endif
-constexpr int kVoteWPC = DLS_VOTE_WPC;  // waves per CU on large models (0: R = 256 per wave)
+constexpr int kVoteWPC = DLS_VOTE_WPC;  // waves per CU on large models (0: 256 groups per wave)
 constexpr int kVoteWPB = DLS_VOTE_WPB;
 static_assert(kVoteWPB >= 1 && kVoteWPB <= kVoteWPBMax, "DLS_VOTE_WPB");
 constexpr int kVoteG = 4;    // widest G (registers: single-buffered 8-client batches)
@@ -264,7 +264,7 @@ template <int CB, bool COUNTS, int G>
 __global__ __launch_bounds__(64 * kVoteWPBMax) void k_sign_vote(
     const uint64_t *__restrict__ planes, int64_t ldp, const int32_t *__restrict__ rows, int K,
     int64_t P, int64_t ngroups, int32_t *__restrict__ counts, float *__restrict__ sign_out,
-    uint64_t *__restrict__ vote_planes, int64_t vote_groups, int64_t rgroups) {
+    uint64_t *__restrict__ vote_planes, int64_t vote_groups, int64_t nwaves) {
     constexpr int B = CB + 3;
     constexpr int NW = COUNTS ? 2 * B + 1 : 3;  // words per group through LDS
     extern __shared__ uint64_t xws[];  // [waves per block][NW][64] (launch: vote_lds)
@@ -272,9 +272,11 @@ __global__ __launch_bounds__(64 * kVoteWPBMax) void k_sign_vote(
     const int lane = __lane_id();
     // the wave's group range [wlo, whi); groups >= ngroups are the zero padding of
     // the last 256-parameter tile (vote 0)
-    const int64_t wlo = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rgroups;
-    if (wlo >= vote_groups) return;  // wave-uniform
-    const int64_t whi = min(wlo + rgroups, vote_groups);
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wave >= nwaves) return;  // wave-uniform
+    // nwaves near-equal ranges (sizes differ by at most one group)
+    const int64_t wlo = wave * vote_groups / nwaves;
+    const int64_t whi = (wave + 1) * vote_groups / nwaves;
     const int64_t gend = min(whi, ngroups);
     HSCounter<CB> cpa[G], cna[G];
     uint64_t nana[G];
@@ -489,28 +491,29 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
     // 2-4 groups per lane (each wave streams R x 16 B of every client row:
     // multi-KB pieces measured 12 % faster than 1 KB at P = 11.2M).  Small
     // models: R = 64, 1 group per lane, double-buffered batches.
-    int64_t R = 64;
+    int64_t nwaves = (vote_groups + 63) / 64;
     int G = 1, wpb = 1;
     if (CB <= 12) {
         if (kVoteWPC > 0) {
+            // exactly kVoteWPC waves per CU, near-equal ranges of up to 64 G groups
             const int64_t waves = (int64_t)kVoteWPC * device_cus();
             const int64_t r = (vote_groups + waves - 1) / waves;
             if (r > 64 && r <= 64 * kVoteG) {
-                R = r;
+                nwaves = waves;
                 G = (int)((r + 63) / 64);
                 wpb = kVoteWPB;
             }
         } else if ((vote_groups + 64 * kVoteG - 1) / (64 * kVoteG) >= 512) {
-            R = 64 * kVoteG;  // the round-3 form: 256 groups per wave, one wave per block
+            // the round-3 form: 256 groups per wave, one wave per block
+            nwaves = (vote_groups + 64 * kVoteG - 1) / (64 * kVoteG);
             G = kVoteG;
         }
     }
-    const int64_t nwaves = (vote_groups + R - 1) / R;
     const dim3 grid((unsigned)((nwaves + wpb - 1) / wpb));
     const size_t lds = (size_t)wpb * (counts ? 2 * (CB + 3) + 1 : 3) * 64 * sizeof(uint64_t);
 #define DLS_VOTE_LAUNCH(C_, G_)                                                                  \
     hipLaunchKernelGGL((k_sign_vote<CB, C_, G_>), grid, dim3(64 * wpb), lds, st, planes, ldp, rows, \
-                       K, P, ngroups, counts, sign_out, vote_planes, vote_groups, R)
+                       K, P, ngroups, counts, sign_out, vote_planes, vote_groups, nwaves)
 #define DLS_VOTE_BY_G(C_)                     \
     switch (G) {                              \
         case 1: DLS_VOTE_LAUNCH(C_, 1); break; \

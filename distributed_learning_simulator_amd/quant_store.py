@@ -31,8 +31,13 @@ FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
 # multi-channel tiles (channel rows a multiple of 16): "adaptive" = the widest of
 # 4 / 2 / 1 KiB that spans at most 3 channel rows (4 KiB for rows >= 2048, 2 KiB
 # for rows >= 1024: every lane's channel constants stay in the kernel's staged
-# table), or a fixed width in elements
-LANE_TILE = "adaptive"
+# table), or a fixed width in elements.  The store keeps one table per mode: the
+# exact kernel is bound by its instruction count at the clock the chip holds
+#  and runs fastest on 1 KiB tiles (4 waves per SIMD); the FMA mode
+# is bound by the stream and runs fastest on the adaptive ones (same-box A/B,
+# 1000 x ResNet-18: exact 2.01 vs 2.21 ms, FMA 1.96 vs 1.88 ms).
+LANE_TILE = 1024  # the exact mode's (and QuantLayout.tiles()' default)
+LANE_TILE_FMA = "adaptive"
 F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
 FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
 QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
@@ -103,9 +108,10 @@ class QuantLayout:
                 return False
         return True
 
-    def tiles(self):
+    def tiles(self, lane_tile=None):
         """(table, nfast): wave tiles; nfast = counts of the 10 grouped kinds at the
         head of the table (dls_hip.h DLS_QTILE_GROUPS), then the general tiles.
+        ``lane_tile``: the multi-channel tiles' width (default LANE_TILE).
 
         * one-channel tiles (groups 0-3: 4, 3, 2, 1 KiB slices): int tensors whose
           channel rows are long (>= 1024, multiple of 64) and fill 1 KiB slices
@@ -138,7 +144,7 @@ class QuantLayout:
                                      j, cend))
                 continue
             if kind and rl % 16 == 0:
-                lt = LANE_TILE
+                lt = LANE_TILE if lane_tile is None else lane_tile
                 if lt == "adaptive":
                     lt = 4096 if rl >= 2048 else (2048 if rl >= 1024 else TILE)
                 for e in range(0, n, lt):
@@ -193,6 +199,9 @@ class QuantizedClientStore:
         t, self.nfast = ql.tiles()
         self.ntiles = len(t)
         self.tiles = torch.from_numpy(t.view(np.uint8).copy()).to(self.device)
+        tf, self.nfast_fma = ql.tiles(LANE_TILE_FMA)
+        self.ntiles_fma = len(tf)
+        self.tiles_fma = torch.from_numpy(tf.view(np.uint8).copy()).to(self.device)
         self._free = list(range(cap))[::-1]
 
     @property
@@ -248,9 +257,16 @@ class QuantizedClientStore:
             total = sum(int(n) for n in ns)
         rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
         w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
-        _native.dequant_fedavg(self.tiles, self.ntiles, self.nfast, self.Q, self.F, self.sz,
-                               rows_t, w_t, float(total), out, mode=mode)
+        tiles, ntiles, nfast = self.table(mode)
+        _native.dequant_fedavg(tiles, ntiles, nfast, self.Q, self.F, self.sz, rows_t, w_t,
+                               float(total), out, mode=mode)
         return out
+
+    def table(self, mode=_native.FEDAVG_EXACT):
+        """(tiles, ntiles, nfast) the fused kernel takes in this mode."""
+        if mode == _native.FEDAVG_FMA:
+            return self.tiles_fma, self.ntiles_fma, self.nfast_fma
+        return self.tiles, self.ntiles, self.nfast
 
     def dequantize(self, row):
         """One client's fp32 dict (the reference's _process_client_parameter output)."""

@@ -11,7 +11,7 @@
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")" && pwd)}"
 TAG="${1:-r02}"
-WLS="${2:-fedavg fedavg1k vote_sign pack quant quant_r18 union gemm bn_act}"
+WLS="${2:-fedavg fedavg1k vote_sign pack quant quant_fma quant_r18 quant_r18_fma union gemm bn_act}"
 OUT="$ROOT/gpurun_out/prof_$TAG"
 RAW="$(mktemp -d /tmp/dlsprof.XXXXXX)"
 LIBDIR="$RAW/lib"

@@ -35,7 +35,10 @@ def test_fed_quant_simulation(tmp_path):
                   "--train_size", "3000", "--test_size", "500")
     assert server.round == 2
     q, scale, zp = server.quantized_parameter
-    assert q.dtype == torch.uint8 and scale.numel() == len(server.prev_model)
+    # the reference's granularity: one quantizer over the concatenated aggregate
+    # (servers/fed_quant_server.py:39): one (scale, zero point), every element once
+    assert q.dtype == torch.uint8 and scale.numel() == 1 and zp.numel() == 1
+    assert q.numel() == sum(v.numel() for v in server.prev_model.values())
 
 
 @pytest.mark.parametrize("algo", ["GTG_shapley_value", "multiround_shapley_value"])

@@ -91,7 +91,8 @@ def setup(dev, want=()):
         pk = torch.empty((16, Wd), dtype=torch.int64, device=dev)
         W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
                      16 * (P * 4 + Wd * 8))
-    if {"quant", "quant1k", "quant_samerow", "quant_w0", "quant_w8", "quant_w16"} & set(want):
+    if {"quant", "quant_fma", "quant1k", "quant_samerow", "quant_w0", "quant_w8",
+            "quant_w16"} & set(want):
         from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
         template = {}
         for name, s in vgg16():
@@ -128,6 +129,11 @@ def setup(dev, want=()):
                                                        st.sz.stride(0) // 2, ptr(rows), ptr(w), 100,
                                                        tot, ptr(qo), stream()),
                         100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+        tf, ntf, nff = st.table(1)  # the FMA mode's tiling (quant_store.LANE_TILE_FMA)
+        W["quant_fma"] = (lambda L: L.dls_dequant_fedavg_mode(
+            ptr(tf), ntf, nfast_arg(L, nff), ptr(st.Q), st.Q.stride(0), ptr(st.F), st.F.stride(0),
+            ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2, ptr(rows), ptr(w), 100, tot, 1,
+            ptr(qo), stream()), 100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
         rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
         from distributed_learning_simulator_amd import quant_store as qs0
         for fwv in (0, 8, 16):
@@ -186,12 +192,16 @@ def setup(dev, want=()):
                 ptr(tdev), len(tt), nfast_arg(L, nft), ptr(sr.Q), sr.Q.stride(0), ptr(sr.F),
                 sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
                 ptr(rows_t), ptr(w_t), rows_t.numel(), tot, mode, ptr(qo18), stream())
-        tab_p, tab_1 = table(saved), table(1024)  # the store's default tiling; 1 KiB lane tiles
+        # the store's tilings (exact: LANE_TILE, FMA: LANE_TILE_FMA), 1 KiB and adaptive
+        tab_p, tab_f = table(saved), table(qs.LANE_TILE_FMA)
+        tab_1, tab_a = table(1024), table("adaptive")
         W["quant_r18"] = (qmode(tab_p, r1k, w1k, t1k, 0), nb, qo18)
         W["quant_r18_l1"] = (qmode(tab_1, r1k, w1k, t1k, 0), nb, qo18)
+        W["quant_r18_a"] = (qmode(tab_a, r1k, w1k, t1k, 0), nb, qo18)
         # DLS_FEDAVG_FMA (1e-6 tolerance mode) on the same 1000 clients
-        W["quant_r18_fma"] = (qmode(tab_p, r1k, w1k, t1k, 1), nb, qo18)
+        W["quant_r18_fma"] = (qmode(tab_f, r1k, w1k, t1k, 1), nb, qo18)
         W["quant_r18_l1_fma"] = (qmode(tab_1, r1k, w1k, t1k, 1), nb, qo18)
+        W["quant_r18_a_fma"] = (qmode(tab_a, r1k, w1k, t1k, 1), nb, qo18)
         # >= 10 ms dispatches for clock / counter probes: the 1000 client rows walked
         # 5 times (K = 5000, every pass from HBM: 11 GB >> L2 + MALL), and the same
         # arithmetic with every client on row 0 (payload loads L2-resident)
@@ -200,25 +210,28 @@ def setup(dev, want=()):
         t5k = float(w5k.sum())
         nb5 = 5 * (nb - 4 * sr.layout.numel) + 4 * sr.layout.numel
         W["quant_r18_k5000"] = (qmode(tab_p, r5k, w5k, t5k, 0), nb5)
-        W["quant_r18_k5000_fma"] = (qmode(tab_p, r5k, w5k, t5k, 1), nb5)
+        W["quant_r18_k5000_fma"] = (qmode(tab_f, r5k, w5k, t5k, 1), nb5)
         W["quant_r18_k5000_l2"] = (qmode(tab_p, torch.zeros_like(r5k), w5k, t5k, 0), nb5)
         tt, nft = tab_p[1], tab_p[2]
-        if "quant_r18_slab" in want:
-            # slab-major emulation: every Q tile of <= 1 KiB gets its own slab of
-            # 1000 consecutive 1 KiB client pieces (ldq = 1 KiB, src = slab start),
-            # so a wave streams its slab sequentially
-            tt, nft = qlr.tiles()
-            ts = tt.copy()
-            isq = np.nonzero(ts["kind"] != 0)[0]
-            ts["src"][isq] = np.arange(len(isq), dtype=np.int64) * 1000 * 1024
-            Qs = torch.empty(len(isq) * 1000 * 1024, dtype=torch.uint8, device=dev)
-            Qs.random_(0, 256, generator=g)
-            tsd = torch.from_numpy(ts.view(np.uint8).copy()).to(dev)
-            W["quant_r18_slab"] = (
-                lambda L: L.dls_dequant_fedavg(
-                    ptr(tsd), len(ts), nfast_arg(L, nft), ptr(Qs), 1024, ptr(sr.F),
-                    sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
-                    ptr(r1k), ptr(w1k), 1000, t1k, ptr(qo18), stream()), nb, qo18)
+        if any(w.startswith("quant_r18_slab") for w in want):
+            # slab-major emulation: every Q tile gets its own slab of 1000 consecutive
+            # T-byte client pieces (ldq = T, src = slab start), so a wave streams its
+            # slab sequentially; T = 1 KiB (1 KiB lane tiles) or 4 KiB (4 KiB lane tiles)
+            for T, tag, lt in ((1024, "", 1024), (4096, "4", "adaptive")):
+                _, tt, nft = table(lt)
+                ts = tt.copy()
+                isq = np.nonzero(ts["kind"] != 0)[0]
+                ts["src"][isq] = np.arange(len(isq), dtype=np.int64) * 1000 * T
+                Qs = torch.empty(len(isq) * 1000 * T, dtype=torch.uint8, device=dev)
+                Qs.random_(0, 256, generator=g)
+                tsd = torch.from_numpy(ts.view(np.uint8).copy()).to(dev)
+                for mode, mtag in ((0, ""), (1, "_fma")):
+                    W[f"quant_r18_slab{tag}{mtag}"] = (
+                        lambda L, tsd=tsd, ts=ts, nft=nft, Qs=Qs, T=T, mode=mode:
+                        L.dls_dequant_fedavg_mode(
+                            ptr(tsd), len(ts), nfast_arg(L, nft), ptr(Qs), T, ptr(sr.F),
+                            sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
+                            ptr(r1k), ptr(w1k), 1000, t1k, mode, ptr(qo18), stream()), nb, qo18)
     # Shapley default path: 50 coalitions (members with p = 1/2) over 50 clients,
     # each client row read once per batch (dls_subset_fedavg_union_f32)
     from distributed_learning_simulator_amd.aggregation import union_batch

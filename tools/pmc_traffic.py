@@ -11,8 +11,11 @@
   gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads,
   so hbm_read = 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B stores.
   With the SQ pass it also carries `valu_busy_frac`: the fraction of the
-  SIMDs' issue cycles the VALU was busy, 4 * SQ_ACTIVE_INST_VALU (quad-cycles,
-  summed over waves) / (1024 SIMDs * GRBM_GUI_ACTIVE / 8) (GRBM_GUI_ACTIVE is
+  SIMDs' issue cycles the VALU was busy, 4 * SQ_ACTIVE_INST_VALU (one count per
+  VALU instruction here, = SQ_INSTS_VALU; 4 SIMD cycles per fp32 wave64
+  instruction, measured: tools/valu_issue_probe.hip — integer / logic ops cost
+  ~2.5, so the fraction overstates integer-heavy kernels such as the sign
+  kernels) / (1024 SIMDs * GRBM_GUI_ACTIVE / 8) (GRBM_GUI_ACTIVE is
   the sum over the 8 XCDs of each dispatch's busy cycles; rocprofv3 serialises
   dispatches while counting, so kernels that run concurrently in the product
   are counted one after another here).
@@ -32,6 +35,7 @@ CALLS = 3
 SIMDS, XCDS = 1024, 8  # MI355X: 256 CUs x 4 SIMDs, 8 XCDs
 KEYS = {"fedavg": "headline", "fedavg1k": "fedavg_k1000", "vote_sign": "sign_vote",
         "pack": "sign_pack", "quant": "fed_quant", "quant_r18": "fed_quant_k1000",
+        "quant_fma": "fed_quant_fma", "quant_r18_fma": "fed_quant_k1000_fma",
         "union": "shapley_exact", "gemm": "shapley_gemm", "bn_act": "bn_act"}
 
 
