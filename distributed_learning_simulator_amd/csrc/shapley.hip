@@ -136,183 +136,6 @@ __global__ __launch_bounds__(kBlock) void k_subset_gemm(const float *__restrict_
     }
 }
 
-// 32 < S <= 32 + kVMax subsets (config 5: S = 50): rows 0..31 on the matrix
-// cores (one 32-row M tile, 4 MFMAs per k-step) and the V = S - 32 remaining
-// rows (rounded up to even) on the VALU in the MFMAs' shadow, instead of a
-// second, mostly empty M tile (64 rows of MFMA work for 50).  Packed fp32 FMA
-// issues 64 flop per SIMD cycle like v_mfma_f32_32x32x2_f32, and the two run
-// side by side.  Lane (h, col) loads U[2s + h][p0 + 4 col .. + 3] for the
-// k-step's MFMA B operand; one v_permlane32_swap per value gives every lane
-// both rows 2s and 2s + 1 of its 4 parameters, and half h accumulates VALU rows
-// 32 + h V/2 + i over ALL clients in client order (an fma chain per element,
-// like the MFMA rows).  C for those rows comes from LDS (Ct[k][32 + v]).
-constexpr int kVMax = 20;
-
-template <int V, bool BETA, int kDepth>
-__global__ __launch_bounds__(kBlock) void k_subset_gemm_mv(const float *__restrict__ C, int64_t ldc,
-                                                           int S, int K,
-                                                           const float *__restrict__ U, int64_t ldu,
-                                                           const int32_t *__restrict__ rows,
-                                                           int64_t P, float *__restrict__ out,
-                                                           int64_t ldo, int64_t ntiles) {
-    static_assert(kNT == 4, "the VALU rows use the 16-byte B operand");
-    static_assert(V % 2 == 0 && V <= kVMax, "VALU rows: an even count");
-    constexpr int HV = V / 2;                      // VALU rows per half-wave
-    constexpr int HVP = (HV + 3) / 4 * 4;          // padded to whole ds_read_b128
-    constexpr int CW = 32 + 2 * HVP;               // Ct row width (rows >= S zero)
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int Kp = ((K + 1) / 2 + kDepth - 1) / kDepth * kDepth * 2;
-    float *Ct = smem;                                             // [Kp][CW]
-    int32_t *srow = reinterpret_cast<int32_t *>(smem + Kp * CW);  // [Kp + 2 kDepth]
-    // Ct[k][i]: i < 32 the MFMA rows; 32 + h HVP + j the VALU row 32 + h HV + j
-    for (int idx = threadIdx.x; idx < Kp * CW; idx += kBlock) {
-        const int k = idx / CW, i = idx % CW;
-        int row = i;
-        if (i >= 32) {
-            const int hh = (i - 32) / HVP, j = (i - 32) % HVP;
-            row = j < HV ? 32 + hh * HV + j : S;  // padding columns read as 0
-        }
-        Ct[idx] = (k < K && row < S) ? C[(int64_t)row * ldc + k] : 0.f;
-    }
-    for (int k = threadIdx.x; k < Kp + 2 * kDepth; k += kBlock) srow[k] = k < K ? rows[k] : -1;
-    __syncthreads();
-
-    const int lane = __lane_id();
-    const int h = lane >> 5, col = lane & 31;
-    const int wave = threadIdx.x >> 6;
-    const int64_t stride = (int64_t)gridDim.x * kWaves;
-    int64_t tile = (int64_t)blockIdx.x * kWaves + wave;
-    if (tile >= ntiles) return;
-    const int nsteps = Kp / 2;
-    const int vrow0 = 32 + h * HV;  // this half's first VALU row
-    const float *cv = Ct + 32 + h * HVP;
-
-    auto loadB = [&](int64_t t, int s) -> f32x4 {
-        const int64_t pp = t * kTileP + 4 * col;
-        const int32_t r = srow[2 * s + h];
-        f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (r >= 0 && t < ntiles && pp + 4 <= P)
-            b = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(U + (int64_t)r * ldu + pp));
-        return b;
-    };
-    f32x4 b[kDepth];
-#pragma unroll
-    for (int i = 0; i < kDepth; ++i) b[i] = loadB(tile, i);
-    for (; tile < ntiles; tile += stride) {
-        const int64_t p = tile * kTileP + 4 * col;
-        const bool inb = p + 4 <= P;
-        const int64_t next = tile + stride;
-        f32x16 acc[4];
-        f32x2 av[HVP][2];  // this half's VALU rows: [j][params (0,1) | (2,3)]
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            if (BETA && inb) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    acc[n][r] = row < S ? out[(int64_t)row * ldo + p + n] : 0.f;
-                }
-            } else {
-                acc[n] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
-                                0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < HV; ++j) {
-            if (BETA && inb && vrow0 + j < S) {
-                const f32x4 o = *reinterpret_cast<const f32x4 *>(out + (int64_t)(vrow0 + j) * ldo + p);
-                av[j][0] = f32x2{o.x, o.y};
-                av[j][1] = f32x2{o.z, o.w};
-            } else {
-                av[j][0] = f32x2{0.f, 0.f};
-                av[j][1] = f32x2{0.f, 0.f};
-            }
-        }
-        auto step = [&](int s, const f32x4 &bb) {
-            const int k = 2 * s + h;
-            const float a = Ct[k * CW + col];
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-                acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bb[n], acc[n], 0, 0, 0);
-            // rows 2s (lanes 0-31) and 2s + 1 (lanes 32-63) of the lane's 4 parameters
-            f32x4 u0, u1;
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(bb[n]),
-                                                                 __float_as_uint(bb[n]), false, false);
-                u0[n] = __uint_as_float(r[0]);
-                u1[n] = __uint_as_float(r[1]);
-            }
-            const f32x2 u0l = f32x2{u0.x, u0.y}, u0h = f32x2{u0.z, u0.w};
-            const f32x2 u1l = f32x2{u1.x, u1.y}, u1h = f32x2{u1.z, u1.w};
-            const float *c0 = cv + (2 * s) * CW, *c1 = cv + (2 * s + 1) * CW;
-#pragma unroll
-            for (int j0 = 0; j0 < HV; j0 += 4) {
-                const f32x4 ca = *reinterpret_cast<const f32x4 *>(c0 + j0);  // client 2s
-                const f32x4 cb = *reinterpret_cast<const f32x4 *>(c1 + j0);  // client 2s + 1
-                const f32x2 ca01 = f32x2{ca.x, ca.y}, ca23 = f32x2{ca.z, ca.w};
-                const f32x2 cb01 = f32x2{cb.x, cb.y}, cb23 = f32x2{cb.z, cb.w};
-                // c broadcast from one half of a register pair (op_sel / op_sel_hi)
-#define DLS_MV_FMA(ACC, C2, B2, SEL)                                                   \
-    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[" SEL ",0,0] op_sel_hi:[" SEL ",1,1]" \
-                 : "+v"(ACC) : "v"(C2), "v"(B2))
-#define DLS_MV_ROW(J, C2A, C2B, SEL)                 \
-    if ((J) < HV) {                                  \
-        DLS_MV_FMA(av[J][0], C2A, u0l, SEL);         \
-        DLS_MV_FMA(av[J][1], C2A, u0h, SEL);         \
-        DLS_MV_FMA(av[J][0], C2B, u1l, SEL);         \
-        DLS_MV_FMA(av[J][1], C2B, u1h, SEL);         \
-    }
-                DLS_MV_ROW(j0, ca01, cb01, "0")
-                DLS_MV_ROW(j0 + 1, ca01, cb01, "1")
-                DLS_MV_ROW(j0 + 2, ca23, cb23, "0")
-                DLS_MV_ROW(j0 + 3, ca23, cb23, "1")
-#undef DLS_MV_ROW
-#undef DLS_MV_FMA
-            }
-        };
-        for (int s = 0; s < nsteps; s += kDepth) {
-            const bool seam = s + kDepth >= nsteps;
-            const int64_t lt = seam ? next : tile;
-            const int ls = seam ? s + kDepth - nsteps : s + kDepth;
-#pragma unroll
-            for (int i = 0; i < kDepth; ++i) {
-                step(s + i, b[i]);
-                b[i] = loadB(lt, ls + i);
-            }
-        }
-        if (inb) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < S) {
-                    f32x4 o;
-#pragma unroll
-                    for (int n = 0; n < 4; ++n) o[n] = acc[n][r];
-                    __builtin_nontemporal_store(o, reinterpret_cast<f32x4 *>(out + (int64_t)row * ldo + p));
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < HV; ++j)
-                if (vrow0 + j < S)
-                    __builtin_nontemporal_store(
-                        f32x4{av[j][0].x, av[j][0].y, av[j][1].x, av[j][1].y},
-                        reinterpret_cast<f32x4 *>(out + (int64_t)(vrow0 + j) * ldo + p));
-        }
-    }
-}
-
-#ifndef DLS_GEMM_MV
-#define DLS_GEMM_MV 1
-#endif
-constexpr bool kGemmMV = DLS_GEMM_MV;  // 32 < S <= 52: MFMA rows + VALU rows
-
-unsigned grid_blocks_of(const void *kern, int64_t ntiles, size_t lds) {
-    const int64_t cap = resident_blocks(kern, kBlock, lds);
-    const int64_t want = (ntiles + kWaves - 1) / kWaves;
-    return (unsigned)(want < cap ? want : cap);
-}
-
 template <int MT, bool BETA, int kDepth>
 unsigned grid_blocks(int64_t ntiles, size_t lds) {
     // exactly the resident blocks (persistent): every wave gets ntiles/(blocks*4) tiles
@@ -348,10 +171,8 @@ extern "C" int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const f
             const int depth = ((steps + 4) / 5 * 5 - steps) < ((steps + 3) / 4 * 4 - steps) ? 5 : 4;
             const int Kp = (steps + depth - 1) / depth * depth * 2;
             const int MT = Sc > 32 ? 2 : 1;
-            const int V = Sc > 32 && Sc <= 32 + kVMax && kGemmMV ? (Sc - 32 + 1) / 2 * 2 : 0;
             const size_t lds =
-                (size_t)Kp * (V ? 32 + 2 * ((V / 2 + 3) / 4 * 4) : 32 * MT) * sizeof(float) +
-                (size_t)(Kp + 2 * depth) * sizeof(int32_t);
+                (size_t)Kp * 32 * MT * sizeof(float) + (size_t)(Kp + 2 * depth) * sizeof(int32_t);
             // C chunk: rows s0.., columns k0.. of the row-major [S, K] matrix (ld K)
             const float *Cc = C + (int64_t)s0 * K + k0;
             const int beta = k0 > 0;
@@ -365,37 +186,11 @@ extern "C" int dls_subset_gemm_f32(const float *C, int32_t S, int32_t K, const f
     else if (MT == 2) DLS_GEMM_LAUNCH(2, false, D_);     \
     else if (beta) DLS_GEMM_LAUNCH(1, true, D_);         \
     else DLS_GEMM_LAUNCH(1, false, D_);
-#define DLS_GEMM_MV_LAUNCH(V_, B_, D_)                                                            \
-    hipLaunchKernelGGL((k_subset_gemm_mv<V_, B_, D_>),                                            \
-                       dim3(grid_blocks_of(reinterpret_cast<const void *>(k_subset_gemm_mv<V_, B_, D_>), \
-                                           ntiles, lds)),                                         \
-                       dim3(kBlock), lds, st, Cc, (int64_t)K, Sc, Kc, U, ldu, rows + k0, P, oc,    \
-                       ldo, ntiles)
-#define DLS_GEMM_MV_V(B_, D_)                             \
-    switch (V) {                                          \
-        case 2: DLS_GEMM_MV_LAUNCH(2, B_, D_); break;     \
-        case 4: DLS_GEMM_MV_LAUNCH(4, B_, D_); break;     \
-        case 6: DLS_GEMM_MV_LAUNCH(6, B_, D_); break;     \
-        case 8: DLS_GEMM_MV_LAUNCH(8, B_, D_); break;     \
-        case 10: DLS_GEMM_MV_LAUNCH(10, B_, D_); break;   \
-        case 12: DLS_GEMM_MV_LAUNCH(12, B_, D_); break;   \
-        case 14: DLS_GEMM_MV_LAUNCH(14, B_, D_); break;   \
-        case 16: DLS_GEMM_MV_LAUNCH(16, B_, D_); break;   \
-        case 18: DLS_GEMM_MV_LAUNCH(18, B_, D_); break;   \
-        default: DLS_GEMM_MV_LAUNCH(20, B_, D_); break;   \
-    }
-            if (V > 0) {
-                if (depth == 5 && beta) DLS_GEMM_MV_V(true, 5)
-                else if (depth == 5) DLS_GEMM_MV_V(false, 5)
-                else if (beta) DLS_GEMM_MV_V(true, 4)
-                else DLS_GEMM_MV_V(false, 4)
-            } else if (depth == 5) {
+            if (depth == 5) {
                 DLS_GEMM_MT_BETA(5)
             } else {
                 DLS_GEMM_MT_BETA(4)
             }
-#undef DLS_GEMM_MV_V
-#undef DLS_GEMM_MV_LAUNCH
 #undef DLS_GEMM_MT_BETA
 #undef DLS_GEMM_LAUNCH
             int rc = check_launch("dls_subset_gemm_f32");

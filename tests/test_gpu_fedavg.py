@@ -117,9 +117,9 @@ def test_subset_exact_batched_matches_oracle():
                                    (70, 300, 2048), (45, 300, 2048 + 64), (52, 17, 4096 + 192),
                                    (33, 2, 640)])
 def test_subset_gemm_mfma_normwise(S, K, P):
-    """fp32 MFMA contraction vs fp64: normwise <= 1e-6 (north-star tolerance).
-    32 < S <= 52 runs 32 rows on MFMA and the rest on the VALU (45 x 300: the
-    running sums of a second client chunk; 52 x 17: odd K, 20 VALU rows; 33: one)."""
+    """fp32 MFMA contraction vs fp64: normwise <= 1e-6 (north-star tolerance);
+    45 x 300: the running sums of a second client chunk; 52 x 17: odd K; 33 x 2:
+    a second M tile of one row."""
     from distributed_learning_simulator_amd import _native
     g = torch.Generator().manual_seed(S * 1000 + K)
     U = torch.randn(K + 3, P, generator=g) * 0.05
