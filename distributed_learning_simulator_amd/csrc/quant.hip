@@ -266,6 +266,9 @@ __device__ __forceinline__ void accum16_fma(float (&acc)[16], u32x4 qv, f32x2 cz
         acc[j + 1] = ra.y;
         acc[j + 8] = rb.x;
         acc[j + 9] = rb.y;
+        // no later conversion is hoisted above this step (hoisting every in-flight
+        // client's conversions costs registers, and with them waves per SIMD)
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -283,7 +286,7 @@ struct QBatch {
     float s[U], z[U], wk[U];
 };
 
-template <bool SIGNED, int G, bool TWO, bool FMA>
+template <bool SIGNED, int G, bool TWO>
 __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8_t *__restrict__ Q,
                                                 const uint32_t (&qoff)[G], int64_t ldq,
                                                 const f32x2 *__restrict__ szc, SzLayout L,
@@ -303,45 +306,6 @@ __device__ __forceinline__ void int_one_channel(float (&acc)[G][16], const uint8
         nsz = szc[(int64_t)cr.r1 * L.row];  // next chunk (its rows landed a chunk ago)
         cr.advance(rows, w, K, base);
         const int n = min(64, K - base);
-        if constexpr (FMA) {
-            // FMA mode: every client of the chunk with zero point 0 -> one
-            // constant per client, fma(q, c, acc) (else the exact path below)
-            if (__ballot(tsz.y != 0.f && __lane_id() < n) == 0) {
-                const float coef = fma_coef(tsz.x, tw, d.b);
-                constexpr int FU = G > 1 ? kQuantUG : kQuantU;  // clients per batch
-                using FB = QBatch<FU, G>;
-                auto ffetch = [&](int j, u32x4 (&qv)[G], float &c) {
-                    const int64_t r = readlane_i(tr, j);
-                    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                        const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);
-#pragma unroll
-                    for (int g = 0; g < G; ++g)
-                        qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
-                    c = readlane_f(coef, j);
-                };
-                auto fstep = [&](const u32x4 (&qv)[G], float c) {
-#pragma unroll
-                    for (int g = 0; g < G; ++g) accum16_fma<SIGNED>(acc[g], qv[g], f32x2{c, c});
-                };
-                chunk_pipeline<FU, FB>(
-                    n,
-                    [&](int j0, FB &bt) {
-#pragma unroll
-                        for (int u = 0; u < FU; ++u) ffetch(j0 + u, bt.qv[u], bt.s[u]);
-                    },
-                    [&](const FB &bt) {
-#pragma unroll
-                        for (int u = 0; u < FU; ++u) fstep(bt.qv[u], bt.s[u]);
-                    },
-                    [&](int j) {
-                        u32x4 qv[G];
-                        float c;
-                        ffetch(j, qv, c);
-                        fstep(qv, c);
-                    });
-                continue;
-            }
-        }
         // one wave-uniform decision per chunk: if every client of the chunk takes
         // the common path (exact fl(z*s) and the fast division), the streaming loop
         // carries that path alone, reading (scale, -fl(z*s)) straight from the table
@@ -656,7 +620,7 @@ __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][1
 // One-channel tiles of up to 4 KiB: slice g of the tile is lanes'
 // 16-element chunks 1024 g + 16 lane; the wave walks the clients once for all
 // its slices (per-client table reads and readlanes amortised over G KiB).
-template <bool SIGNED, int G, bool TWO, bool FMA>
+template <bool SIGNED, int G, bool TWO>
 __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                           int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                           const int32_t *__restrict__ rows,
@@ -672,8 +636,7 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
         // idle lanes load a valid duplicate (loads stay unconditional)
         qoff[g] = (uint32_t)(wt.t.src + (e0 < wt.lenpad ? e0 : wt.lenpad - 16));  // ldq < 4 GiB
     }
-    int_one_channel<SIGNED, G, TWO, FMA>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K,
-                                         d);
+    int_one_channel<SIGNED, G, TWO>(acc, Q, qoff, ldq, sz + wt.t.chan0 * L.chan, L, rows, w, K, d);
     store_tile<G>(wt, acc, out);
 }
 
@@ -697,7 +660,7 @@ __device__ __forceinline__ void fast_tile(const WaveTile &wt, const uint8_t *__r
 // lane with each client's payload and the check per client.
 constexpr int kSpanMax = 4;
 
-template <bool SIGNED, int G, bool TWO, bool FMA>
+template <bool SIGNED, int G, bool TWO>
 __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                           int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                           const int32_t *__restrict__ rows,
@@ -759,17 +722,7 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         cr.advance(rows, w, K, base);
         const int n = min(64, K - base);
         bool allfast = false;
-        if (staged && FMA) {
-            // FMA mode: every (client, channel) of the chunk with zero point 0
-            // (symmetric int8) accumulates fma(q, c, acc), c = fl(fl(s * n_i) / N)
-            int ok = 1;
-#pragma unroll
-            for (int c = 0; c < kSpanMax; ++c) {
-                ok &= (int)(c >= span) | (int)(tsz[c].y == 0.f);
-                tab[c][__lane_id()] = f32x2{fma_coef(tsz[c].x, tw, d.b), 0.f};
-            }
-            allfast = __ballot(!ok && __lane_id() < n) == 0;
-        } else if (staged) {
+        if (staged) {
             // every (client, channel) of the chunk on the common path: exact fl(z*s)
             // and the fast division range (always, for symmetric int8)
             int ok = d.fast;
@@ -794,18 +747,14 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
                 b.j = j;
             };
             auto sstep = [&](const SOne &b) {
-                // the lane's (s, -zs) or FMA constant: a broadcast LDS read (<= kSpanMax
-                // addresses per wave)
+                // the lane's (s, -zs): a broadcast LDS read (<= kSpanMax addresses per wave)
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    if constexpr (DLS_QUANT_PROBE == 1) {
+                    if constexpr (DLS_QUANT_PROBE == 1)
                         acc[g][g] += __uint_as_float((b.qv[g].x ^ b.qv[g].y ^ b.qv[g].z ^ b.qv[g].w) &
                                                      0x3fffffffu);
-                    } else if constexpr (FMA) {
-                        accum16_fma<SIGNED>(acc[g], b.qv[g], tab[0][toff[g] + b.j]);
-                    } else {
+                    else
                         accum16_pk<SIGNED, TWO>(acc[g], b.qv[g], tab[0][toff[g] + b.j], b.wk, d);
-                    }
                 }
             };
             chunk_pipeline_1tail<US, SBatch>(
@@ -894,19 +843,285 @@ __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][1
     }
 }
 
-template <int G, bool TWO, bool FMA>
+template <int G, bool TWO>
 __global__ __launch_bounds__(kBlock, 1) void k_dequant_fast(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
     const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
-    // one launch per (slice count G, division method, mode): each instance has
-    // its own register budget
+    // one launch per (slice count G, division method): each instance has its
+    // own register budget
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
     if (wt.t.kind == 1)
-        fast_tile<true, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        fast_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
     else
-        fast_tile<false, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        fast_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+}
+
+// ------------------------------------------------------------ FMA mode
+// DLS_FEDAVG_FMA (north-star FedAvg tolerance, not bit-exact): every int
+// element accumulates fma(q - z, c, acc) with one constant per (client,
+// channel) c = fl(fl(s * n_i) / N) (q - z is exact in fp32).  None of the exact
+// path's rounding sequence, range checks or fallbacks is needed, so these
+// kernels are lean (no rare path in the register budget): more waves per SIMD,
+// more bytes in flight.  Zero points are almost always 0 (symmetric qint8, the
+// QAT worker's format): a chunk whose zero points are all 0 skips the
+// subtraction (one wave-uniform test per 64-client chunk).
+template <bool SEXT>
+__device__ __forceinline__ void accum16_fmaz(float (&acc)[16], u32x4 qv, f32x2 cz) {
+    // cz = (c, -z): x + (-z) exact, then fma(x, c, acc)
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+        const int k = j & 3;
+        f32x2 xa = f32x2{byte_val<SEXT>(qv[j >> 2], k), byte_val<SEXT>(qv[j >> 2], k + 1)};
+        f32x2 xb = f32x2{byte_val<SEXT>(qv[(j >> 2) + 2], k), byte_val<SEXT>(qv[(j >> 2) + 2], k + 1)};
+        f32x2 ra = f32x2{acc[j], acc[j + 1]}, rb = f32x2{acc[j + 8], acc[j + 9]};
+        asm volatile(
+            "v_pk_add_f32 %[xa], %[xa], %[cz] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_pk_add_f32 %[xb], %[xb], %[cz] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+            "v_pk_fma_f32 %[ra], %[xa], %[cz], %[ra] op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %[rb], %[xb], %[cz], %[rb] op_sel_hi:[1,0,1]"
+            : [ra] "+v"(ra), [rb] "+v"(rb), [xa] "+v"(xa), [xb] "+v"(xb)
+            : [cz] "v"(cz));
+        acc[j] = ra.x;
+        acc[j + 1] = ra.y;
+        acc[j + 8] = rb.x;
+        acc[j + 9] = rb.y;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <bool SEXT>
+__device__ __forceinline__ void accum16_fma_any(float (&acc)[16], u32x4 qv, f32x2 cz, bool allz) {
+    if (allz)
+        accum16_fma<SEXT>(acc, qv, cz);
+    else
+        accum16_fmaz<SEXT>(acc, qv, cz);
+}
+
+// One-channel tiles (groups 0-3) in FMA mode: one (c, -z) per client, read back
+// as wave-uniform values; G KiB slices per client.
+template <bool SIGNED, int G>
+__device__ __forceinline__ void fma_one_channel_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
+                                                     int64_t ldq, const f32x2 *__restrict__ sz,
+                                                     SzLayout L, const int32_t *__restrict__ rows,
+                                                     const float *__restrict__ w, int K, float N,
+                                                     float *__restrict__ out) {
+    float acc[G][16];
+    uint32_t qoff[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[g][e] = 0.f;
+        const int e0 = 1024 * g + 16 * __lane_id();
+        qoff[g] = (uint32_t)(wt.t.src + (e0 < wt.lenpad ? e0 : wt.lenpad - 16));
+    }
+    const f32x2 *szc = sz + wt.t.chan0 * L.chan;
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    f32x2 nsz = szc[(int64_t)cr.r0 * L.row];
+    constexpr int U = G > 1 ? kQuantUG : kQuantU;
+    struct B {
+        u32x4 qv[U][G];
+        float c[U], z[U];
+    };
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float coef = fma_coef(nsz.x, cr.w0, N), nz = -nsz.y;
+        const bool allz = __ballot(nsz.y != 0.f && __lane_id() < K - base) == 0;
+        nsz = szc[(int64_t)cr.r1 * L.row];  // next chunk (its rows landed a chunk ago)
+        cr.advance(rows, w, K, base);
+        const int n = min(64, K - base);
+        auto fetch = [&](int j, u32x4 (&qv)[G], float &c, float &z) {
+            const int64_t r = readlane_i(tr, j);
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+            c = readlane_f(coef, j);
+            z = readlane_f(nz, j);
+        };
+        auto step = [&](const u32x4 (&qv)[G], float c, float z) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) accum16_fma_any<SIGNED>(acc[g], qv[g], f32x2{c, z}, allz);
+        };
+        chunk_pipeline<U, B>(
+            n,
+            [&](int j0, B &b) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) fetch(j0 + u, b.qv[u], b.c[u], b.z[u]);
+            },
+            [&](const B &b) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) step(b.qv[u], b.c[u], b.z[u]);
+            },
+            [&](int j) {
+                u32x4 qv[G];
+                float c, z;
+                fetch(j, qv, c, z);
+                step(qv, c, z);
+            });
+    }
+    store_tile<G>(wt, acc, out);
+}
+
+// Multi-channel (lane) tiles (groups 4-7) in FMA mode: the tile's <= kSpanMax
+// channels' (c, -z) of the chunk's 64 clients staged in the wave's LDS table
+// (lane j computes client j's), one broadcast ds_read_b64 per slice and client.
+// Tiles over more channels gather each lane's (scale, zero point) per client,
+// one KiB slice at a time.
+template <bool SIGNED, int G>
+__device__ __forceinline__ void fma_lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
+                                              int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
+                                              const int32_t *__restrict__ rows,
+                                              const float *__restrict__ w, int K, float N,
+                                              float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) f32x2 ftab[kBlock / 64][kSpanMax][64];
+    f32x2(*tab)[64] = ftab[threadIdx.x >> 6];
+    float acc[G][16];
+    uint32_t qoff[G], toff[G];
+    int64_t coff[G];
+    const int span = (wt.t.row_pos + wt.t.len - 1) / wt.t.row_len + 1;  // wave-uniform
+    const bool staged = span <= kSpanMax;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[g][e] = 0.f;
+        const int e0 = 1024 * g + 16 * __lane_id();
+        const int ec = e0 < wt.lenpad ? e0 : wt.lenpad - 16;
+        qoff[g] = (uint32_t)(wt.t.src + ec);
+        const int crel = min((wt.t.row_pos + ec) / wt.t.row_len, span - 1);
+        coff[g] = (int64_t)min(wt.t.chan0 + crel, wt.t.chan_end - 1) * L.chan;
+        toff[g] = (uint32_t)min(crel, kSpanMax - 1) * 64;
+    }
+    auto tab_load = [&](int r, f32x2 (&v)[kSpanMax]) {
+#pragma unroll
+        for (int c = 0; c < kSpanMax; ++c)
+            v[c] = sz[(int64_t)min(wt.t.chan0 + c, wt.t.chan_end - 1) * L.chan + (int64_t)r * L.row];
+    };
+    constexpr int US = G > 1 ? kLaneUSG : kLaneUS;
+    struct SOne {
+        u32x4 qv[G];
+        int j;
+    };
+    struct SBatch {
+        SOne c[US];
+    };
+    ChunkRows cr;
+    cr.init(rows, w, K);
+    f32x2 nsz[kSpanMax];
+    if (staged) tab_load(cr.r0, nsz);
+    for (int base = 0; base < K; base += 64) {
+        const int tr = cr.r0;
+        const float tw = cr.w0;
+        const int n = min(64, K - base);
+        if (staged) {
+            int z0 = 1;
+#pragma unroll
+            for (int c = 0; c < kSpanMax; ++c) {
+                z0 &= (int)(c >= span) | (int)(nsz[c].y == 0.f);
+                tab[c][__lane_id()] = f32x2{fma_coef(nsz[c].x, tw, N), -nsz[c].y};
+            }
+            const bool allz = __ballot(!z0 && __lane_id() < n) == 0;
+            tab_load(cr.r1, nsz);  // next chunk (its rows landed a chunk ago)
+            cr.advance(rows, w, K, base);
+            auto sfetch = [&](int j, SOne &b) {
+                const int64_t r = readlane_i(tr, j);
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+                b.j = j;
+            };
+            auto sstep = [&](const SOne &b) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if constexpr (DLS_QUANT_PROBE == 1)
+                        acc[g][g] += __uint_as_float((b.qv[g].x ^ b.qv[g].y ^ b.qv[g].z ^ b.qv[g].w) &
+                                                     0x3fffffffu);
+                    else
+                        accum16_fma_any<SIGNED>(acc[g], b.qv[g], tab[0][toff[g] + b.j], allz);
+                }
+            };
+            chunk_pipeline_1tail<US, SBatch>(
+                n,
+                [&](int j0, SBatch &b) {
+#pragma unroll
+                    for (int u = 0; u < US; ++u) sfetch(j0 + u, b.c[u]);
+                },
+                [&](const SBatch &b) {
+#pragma unroll
+                    for (int u = 0; u < US; ++u) sstep(b.c[u]);
+                },
+                [&](int j) {
+                    SOne b;
+                    sfetch(j, b);
+                    sstep(b);
+                });
+            continue;
+        }
+        cr.advance(rows, w, K, base);
+        // more than kSpanMax channels: each lane's (scale, zero point) per client
+        struct One1 {
+            u32x4 qv;
+            f32x2 s;
+            float wk;
+        };
+        auto rare = [&](auto g_c) {
+            constexpr int g = decltype(g_c)::value;
+            auto fetch = [&](int j, One1 &b) {
+                const int64_t r = readlane_i(tr, j);
+                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+                b.qv = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+                b.s = sz[coff[g] + r * L.row];
+                b.wk = readlane_f(tw, j);
+            };
+            auto step = [&](const One1 &b) {
+                accum16_fmaz<SIGNED>(acc[g], b.qv, f32x2{fma_coef(b.s.x, b.wk, N), -b.s.y});
+            };
+            chunk_pipeline<1, One1>(
+                n, [&](int j0, One1 &bb) { fetch(j0, bb); }, [&](const One1 &bb) { step(bb); },
+                [&](int j) {
+                    One1 bb;
+                    fetch(j, bb);
+                    step(bb);
+                });
+        };
+        rare(std::integral_constant<int, 0>{});
+        if constexpr (G > 1) rare(std::integral_constant<int, 1>{});
+        if constexpr (G > 2) rare(std::integral_constant<int, 2>{});
+        if constexpr (G > 3) rare(std::integral_constant<int, 3>{});
+    }
+    store_tile<G>(wt, acc, out);
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_dequant_fast_fma(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
+    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
+    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    if (wt.t.kind == 1)
+        fma_one_channel_tile<true, G>(wt, Q, ldq, sz, L, rows, w, K, d.b, out);
+    else
+        fma_one_channel_tile<false, G>(wt, Q, ldq, sz, L, rows, w, K, d.b, out);
+}
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_dequant_lanes_fma(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
+    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
+    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    if (wt.t.kind == 1)
+        fma_lane_tile<true, G>(wt, Q, ldq, sz, L, rows, w, K, d.b, out);
+    else
+        fma_lane_tile<false, G>(wt, Q, ldq, sz, L, rows, w, K, d.b, out);
 }
 
 // fp32 tensors (biases, norm weights) as their own group: tiles of <= 256
@@ -1084,7 +1299,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_small(const dls_qtile *__res
     }
 }
 
-template <int G, bool TWO, bool FMA>
+template <int G, bool TWO>
 __global__ __launch_bounds__(kBlock, 1) void k_dequant_lanes(
     const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
     const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
@@ -1092,9 +1307,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_dequant_lanes(
     WaveTile wt;
     if (!wave_tile(tiles, ntiles, wt)) return;
     if (wt.t.kind == 1)
-        lane_tile<true, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        lane_tile<true, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
     else
-        lane_tile<false, G, TWO, FMA>(wt, Q, ldq, sz, L, rows, w, K, d, out);
+        lane_tile<false, G, TWO>(wt, Q, ldq, sz, L, rows, w, K, d, out);
 }
 
 __global__ __launch_bounds__(kBlock) void k_dequant_general(
@@ -1399,22 +1614,14 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
                          const int32_t *, const float *, int, FastDiv, float *);
     // [group][0: Markstein, 1: two-constant division, 2: FMA mode]
     static const Kfn kgroup[8][3] = {
-        {k_dequant_fast<4, false, false>, k_dequant_fast<4, true, false>,
-         k_dequant_fast<4, false, true>},
-        {k_dequant_fast<3, false, false>, k_dequant_fast<3, true, false>,
-         k_dequant_fast<3, false, true>},
-        {k_dequant_fast<2, false, false>, k_dequant_fast<2, true, false>,
-         k_dequant_fast<2, false, true>},
-        {k_dequant_fast<1, false, false>, k_dequant_fast<1, true, false>,
-         k_dequant_fast<1, false, true>},
-        {k_dequant_lanes<4, false, false>, k_dequant_lanes<4, true, false>,
-         k_dequant_lanes<4, false, true>},
-        {k_dequant_lanes<3, false, false>, k_dequant_lanes<3, true, false>,
-         k_dequant_lanes<3, false, true>},
-        {k_dequant_lanes<2, false, false>, k_dequant_lanes<2, true, false>,
-         k_dequant_lanes<2, false, true>},
-        {k_dequant_lanes<1, false, false>, k_dequant_lanes<1, true, false>,
-         k_dequant_lanes<1, false, true>}};
+        {k_dequant_fast<4, false>, k_dequant_fast<4, true>, k_dequant_fast_fma<4>},
+        {k_dequant_fast<3, false>, k_dequant_fast<3, true>, k_dequant_fast_fma<3>},
+        {k_dequant_fast<2, false>, k_dequant_fast<2, true>, k_dequant_fast_fma<2>},
+        {k_dequant_fast<1, false>, k_dequant_fast<1, true>, k_dequant_fast_fma<1>},
+        {k_dequant_lanes<4, false>, k_dequant_lanes<4, true>, k_dequant_lanes_fma<4>},
+        {k_dequant_lanes<3, false>, k_dequant_lanes<3, true>, k_dequant_lanes_fma<3>},
+        {k_dequant_lanes<2, false>, k_dequant_lanes<2, true>, k_dequant_lanes_fma<2>},
+        {k_dequant_lanes<1, false>, k_dequant_lanes<1, true>, k_dequant_lanes_fma<1>}};
     // A wave walks all K clients, so waves are long and equal: a group is launched
     // in pieces of at most one generation of resident waves (a last generation of
     // a few waves would run alone at latency-bound speed; cf. dls_fedavg_f32).

@@ -204,12 +204,13 @@ int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nf
                        int64_t sz_chan, const int32_t *rows, const float *weight, int32_t K,
                        float total, float *out, dls_stream_t stream);
 /* The same with a mode (DLS_FEDAVG_EXACT: dls_dequant_fedavg, bit-exact;
- * DLS_FEDAVG_FMA: the int tiles whose zero points are 0 (symmetric qint8, the
- * QAT worker's format) accumulate out = fma(q, c, out) with one constant per
- * (client, channel) c = fl(fl(scale * n_i) / N) — one packed op per element
- * pair instead of five, a different rounding of each term: within the
- * north-star's 1e-6 FedAvg tolerance (normwise), not bit-exact; every other
- * tile runs its exact kernel). */
+ * DLS_FEDAVG_FMA: the int tiles of groups 0-7 accumulate out = fma(q - zp, c,
+ * out) with one constant per (client, channel) c = fl(fl(scale * n_i) / N)
+ * (q - zp exact; the subtraction skipped for chunks of zero points 0, the QAT
+ * worker's symmetric qint8) — one packed op per element pair instead of five,
+ * a different rounding of each term: within the north-star's 1e-6 FedAvg
+ * tolerance (normwise), not bit-exact; groups 8-9 and the general tiles run
+ * their exact kernels). */
 int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast,
                             const void *Q, int64_t ldq, const float *F, int64_t ldf,
                             const float *sz, int64_t sz_row, int64_t sz_chan, const int32_t *rows,

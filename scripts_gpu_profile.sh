@@ -8,6 +8,7 @@
 # Only the stats CSVs and the counter rows of this library's kernels are kept,
 # under gpurun_out/prof_<tag>/; tools/pmc_traffic.py summarises them.
 #   scripts_gpu_profile.sh <tag> [workloads]
+# PROFILE_PARTS="traces" / "pmc" runs only that part (a gpurun call is capped at 20 min).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")" && pwd)}"
 TAG="${1:-r02}"
@@ -32,12 +33,16 @@ keep_counters() {  # $1 = pass name: header + rows of dls:: kernels only
     fi
     rm -rf "$RAW/$1"
 }
+PARTS="${PROFILE_PARTS:-traces pmc}"
+if [[ "$PARTS" == *traces* ]]; then
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/trace_headline" -o run -- \
     python3 "$ROOT/bench.py" --steps 20 --warmup 5 --only headline > "$OUT/trace_headline.json" 2> "$OUT/trace_headline.log" || exit $?
 keep_stats trace_headline
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/trace" -o run -- \
     python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --evals 2 > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.log" || exit $?
 keep_stats trace
+fi
+[[ "$PARTS" == *pmc* ]] || { rm -rf "$RAW"; echo "profiles in $OUT"; exit 0; }
 for W in $WLS; do
     for C in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"; do
         P="pmc_${W}_$(echo $C | cut -d' ' -f1)"
