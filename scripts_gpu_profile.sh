@@ -39,7 +39,9 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/
     python3 "$ROOT/bench.py" --steps 20 --warmup 5 --only headline > "$OUT/trace_headline.json" 2> "$OUT/trace_headline.log" || exit $?
 keep_stats trace_headline
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$RAW/trace" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --evals 2 > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.log" || exit $?
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline \
+    --only headline,fedavg_k1000,sign_vote,fed_quant,fed_quant_k1000,shapley_exact,shapley_gemm \
+    > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.log" || exit $?
 keep_stats trace
 fi
 [[ "$PARTS" == *pmc* ]] || { rm -rf "$RAW"; echo "profiles in $OUT"; exit 0; }
