@@ -77,8 +77,10 @@ def main(tag):
             if sq.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in sq:
                 busy = 4 * sq["SQ_ACTIVE_INST_VALU"] / (SIMDS * sq["GRBM_GUI_ACTIVE"] / XCDS)
                 out_json[key]["valu_busy_frac"] = busy
-                lines.append(f"    VALU busy {busy:.3f} of the SIMDs' cycles "
-                             f"(4 x SQ_ACTIVE_INST_VALU / (1024 x GRBM_GUI_ACTIVE / 8))")
+                lines.append(f"    VALU issue {busy:.3f} at the fp32 cost (4 x SQ_ACTIVE_INST_VALU / (1024 x "
+                             f"GRBM_GUI_ACTIVE / 8); 4 cycles per fp32 wave64 instruction, integer / "
+                             f"logic forms ~2.5, so integer-heavy kernels can exceed 1: "
+                             f"profiles/r04a_valu_issue.txt)")
         except OSError:
             pass
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fo:
