@@ -278,6 +278,8 @@ __device__ __forceinline__ float fma_coef(float s, float wk, float N) { return (
 
 #ifndef DLS_QUANT_PROBE
 #define DLS_QUANT_PROBE 0  // 1: stream-only timing probe (loads + a xor per dword; wrong output)
+// 2: as 1, and lane_tile skips its per-chunk scale staging (no sz gathers, LDS table, ballot)
+// 3: as 2, and lane_tile addresses client j of a chunk as row base + j (no v_readlane)
 #endif
 
 template <int U, int GN>
@@ -711,18 +713,18 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
     ChunkRows cr;
     cr.init(rows, w, K);
     f32x2 nsz[kSpanMax];
-    if (staged) tab_load(cr.r0, nsz);
+    if (staged && DLS_QUANT_PROBE < 2) tab_load(cr.r0, nsz);
     for (int base = 0; base < K; base += 64) {
         const int tr = cr.r0;
         const float tw = cr.w0;
         f32x2 tsz[kSpanMax];
 #pragma unroll
         for (int c = 0; c < kSpanMax; ++c) tsz[c] = nsz[c];
-        if (staged) tab_load(cr.r1, nsz);  // next chunk (its rows landed a chunk ago)
+        if (staged && DLS_QUANT_PROBE < 2) tab_load(cr.r1, nsz);  // next chunk (its rows landed a chunk ago)
         cr.advance(rows, w, K, base);
         const int n = min(64, K - base);
-        bool allfast = false;
-        if (staged) {
+        bool allfast = DLS_QUANT_PROBE >= 2;
+        if (staged && DLS_QUANT_PROBE < 2) {
             // every (client, channel) of the chunk on the common path: exact fl(z*s)
             // and the fast division range (always, for symmetric int8)
             int ok = d.fast;
@@ -737,20 +739,20 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
         }
         if (allfast) {
             auto sfetch = [&](int j, SOne &b) {
-                const int64_t r = readlane_i(tr, j);
+                const int64_t r = DLS_QUANT_PROBE >= 3 ? (int64_t)(base + j) : readlane_i(tr, j);
                 const auto rs = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
 #pragma unroll
                 for (int g = 0; g < G; ++g)
                     b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
-                b.wk = readlane_f(tw, j);
+                b.wk = DLS_QUANT_PROBE >= 3 ? 1.f : readlane_f(tw, j);
                 b.j = j;
             };
             auto sstep = [&](const SOne &b) {
                 // the lane's (s, -zs): a broadcast LDS read (<= kSpanMax addresses per wave)
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    if constexpr (DLS_QUANT_PROBE == 1)
+                    if constexpr (DLS_QUANT_PROBE >= 1)
                         acc[g][g] += __uint_as_float((b.qv[g].x ^ b.qv[g].y ^ b.qv[g].z ^ b.qv[g].w) &
                                                      0x3fffffffu);
                     else
@@ -966,24 +968,32 @@ __device__ __forceinline__ void fma_one_channel_tile(const WaveTile &wt, const u
     store_tile<G>(wt, acc, out);
 }
 
-// Multi-channel (lane) tiles (groups 4-7) in FMA mode: the tile's <= kSpanMax
-// channels' (c, -z) of the chunk's 64 clients staged in the wave's LDS table
-// (lane j computes client j's), one broadcast ds_read_b64 per slice and client.
-// Tiles over more channels gather each lane's (scale, zero point) per client,
-// one KiB slice at a time.
+// Multi-channel (lane) tiles (groups 4-7) in FMA mode: the channels' (c, -z) of
+// the chunk's 64 clients staged in the wave's LDS table (lane j computes client
+// j's), one broadcast ds_read_b64 per slice and client.  A tile over more than
+// kSpanMax channels is walked in ceil(span / kSpanMax) passes of kSpanMax
+// channels; a lane outside the pass's channels reads the table's zero row
+// (c = 0: fma(x, 0, acc) leaves acc), so there is ONE walk loop.  A second loop
+// (the per-client gather path of round 3), or a per-chunk choice between the
+// zero-point forms, made the register allocator keep two copies of the
+// accumulators: 234 VGPRs at G = 4 (2 waves per SIMD, the group in two launch
+// pieces of 1.2 waves per SIMD) against 156 with one loop (3 waves per SIMD,
+// one piece).  The zero point is always subtracted: x + (-z) is exact and
+// x + (-0) == x, so a chunk of zero points 0 gives the bits of the
+// subtraction-free form.
 template <bool SIGNED, int G>
 __device__ __forceinline__ void fma_lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                               int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                               const int32_t *__restrict__ rows,
                                               const float *__restrict__ w, int K, float N,
                                               float *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) f32x2 ftab[kBlock / 64][kSpanMax][64];
+    __shared__ __attribute__((aligned(16))) f32x2 ftab[kBlock / 64][kSpanMax + 1][64];
     f32x2(*tab)[64] = ftab[threadIdx.x >> 6];
+    tab[kSpanMax][__lane_id()] = f32x2{0.f, 0.f};  // the zero row
     float acc[G][16];
-    uint32_t qoff[G], toff[G];
-    int64_t coff[G];
+    uint32_t qoff[G];
+    int crel[G];  // the lane's channel in slice g, relative to the tile's first
     const int span = (wt.t.row_pos + wt.t.len - 1) / wt.t.row_len + 1;  // wave-uniform
-    const bool staged = span <= kSpanMax;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
 #pragma unroll
@@ -991,15 +1001,8 @@ __device__ __forceinline__ void fma_lane_tile(const WaveTile &wt, const uint8_t 
         const int e0 = 1024 * g + 16 * __lane_id();
         const int ec = e0 < wt.lenpad ? e0 : wt.lenpad - 16;
         qoff[g] = (uint32_t)(wt.t.src + ec);
-        const int crel = min((wt.t.row_pos + ec) / wt.t.row_len, span - 1);
-        coff[g] = (int64_t)min(wt.t.chan0 + crel, wt.t.chan_end - 1) * L.chan;
-        toff[g] = (uint32_t)min(crel, kSpanMax - 1) * 64;
+        crel[g] = min((wt.t.row_pos + ec) / wt.t.row_len, span - 1);
     }
-    auto tab_load = [&](int r, f32x2 (&v)[kSpanMax]) {
-#pragma unroll
-        for (int c = 0; c < kSpanMax; ++c)
-            v[c] = sz[(int64_t)min(wt.t.chan0 + c, wt.t.chan_end - 1) * L.chan + (int64_t)r * L.row];
-    };
     constexpr int US = G > 1 ? kLaneUSG : kLaneUS;
     struct SOne {
         u32x4 qv[G];
@@ -1008,92 +1011,81 @@ __device__ __forceinline__ void fma_lane_tile(const WaveTile &wt, const uint8_t 
     struct SBatch {
         SOne c[US];
     };
+    // passes x chunks as ONE loop (a loop over passes around the chunk loop cost
+    // 24 VGPRs at G = 4); almost every tile has one pass
+    const int npass = (span + kSpanMax - 1) / kSpanMax;
+    const int nch = (K + 63) / 64;
+    int c0 = wt.t.chan0;  // the pass's first channel
+    uint32_t toff[G];     // the lane's table row, in pairs
+    auto pass_rows = [&](int p) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int c = crel[g] - kSpanMax * p;
+            toff[g] = (uint32_t)(c >= 0 && c < kSpanMax ? c : kSpanMax) * 64;
+        }
+    };
+    auto tab_load = [&](int r, f32x2 (&v)[kSpanMax]) {
+#pragma unroll
+        for (int c = 0; c < kSpanMax; ++c)
+            v[c] = sz[(int64_t)min(c0 + c, wt.t.chan_end - 1) * L.chan + (int64_t)r * L.row];
+    };
+    pass_rows(0);
     ChunkRows cr;
     cr.init(rows, w, K);
     f32x2 nsz[kSpanMax];
-    if (staged) tab_load(cr.r0, nsz);
-    for (int base = 0; base < K; base += 64) {
+    tab_load(cr.r0, nsz);
+    for (int it = 0, p = 0, base = 0; it < npass * nch; ++it) {
         const int tr = cr.r0;
         const float tw = cr.w0;
         const int n = min(64, K - base);
-        if (staged) {
-            int z0 = 1;
 #pragma unroll
-            for (int c = 0; c < kSpanMax; ++c) {
-                z0 &= (int)(c >= span) | (int)(nsz[c].y == 0.f);
-                tab[c][__lane_id()] = f32x2{fma_coef(nsz[c].x, tw, N), -nsz[c].y};
-            }
-            const bool allz = __ballot(!z0 && __lane_id() < n) == 0;
-            tab_load(cr.r1, nsz);  // next chunk (its rows landed a chunk ago)
-            cr.advance(rows, w, K, base);
-            auto sfetch = [&](int j, SOne &b) {
-                const int64_t r = readlane_i(tr, j);
-                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
-                b.j = j;
-            };
-            auto sstep = [&](const SOne &b) {
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    if constexpr (DLS_QUANT_PROBE == 1)
-                        acc[g][g] += __uint_as_float((b.qv[g].x ^ b.qv[g].y ^ b.qv[g].z ^ b.qv[g].w) &
-                                                     0x3fffffffu);
-                    else
-                        accum16_fma_any<SIGNED>(acc[g], b.qv[g], tab[0][toff[g] + b.j], allz);
-                }
-            };
-            chunk_pipeline_1tail<US, SBatch>(
-                n,
-                [&](int j0, SBatch &b) {
-#pragma unroll
-                    for (int u = 0; u < US; ++u) sfetch(j0 + u, b.c[u]);
-                },
-                [&](const SBatch &b) {
-#pragma unroll
-                    for (int u = 0; u < US; ++u) sstep(b.c[u]);
-                },
-                [&](int j) {
-                    SOne b;
-                    sfetch(j, b);
-                    sstep(b);
-                });
-            continue;
-        }
+        for (int c = 0; c < kSpanMax; ++c)
+            tab[c][__lane_id()] = f32x2{fma_coef(nsz[c].x, tw, N), -nsz[c].y};
+        tab_load(cr.r1, nsz);  // next chunk (its rows landed a chunk ago)
         cr.advance(rows, w, K, base);
-        // more than kSpanMax channels: each lane's (scale, zero point) per client
-        struct One1 {
-            u32x4 qv;
-            f32x2 s;
-            float wk;
+        auto sfetch = [&](int j, SOne &b) {
+            const int64_t r = readlane_i(tr, j);
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                b.qv[g] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
+            b.j = j;
         };
-        auto rare = [&](auto g_c) {
-            constexpr int g = decltype(g_c)::value;
-            auto fetch = [&](int j, One1 &b) {
-                const int64_t r = readlane_i(tr, j);
-                const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t *>(Q + r * ldq), 0, (int)0xffffffffu, 0x00020000);  // 4 GiB
-                b.qv = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)qoff[g], 0, 2 /* nt */);
-                b.s = sz[coff[g] + r * L.row];
-                b.wk = readlane_f(tw, j);
-            };
-            auto step = [&](const One1 &b) {
-                accum16_fmaz<SIGNED>(acc[g], b.qv, f32x2{fma_coef(b.s.x, b.wk, N), -b.s.y});
-            };
-            chunk_pipeline<1, One1>(
-                n, [&](int j0, One1 &bb) { fetch(j0, bb); }, [&](const One1 &bb) { step(bb); },
-                [&](int j) {
-                    One1 bb;
-                    fetch(j, bb);
-                    step(bb);
-                });
+        auto sstep = [&](const SOne &b) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                if constexpr (DLS_QUANT_PROBE == 1)
+                    acc[g][g] += __uint_as_float((b.qv[g].x ^ b.qv[g].y ^ b.qv[g].z ^ b.qv[g].w) &
+                                                 0x3fffffffu);
+                else
+                    accum16_fmaz<SIGNED>(acc[g], b.qv[g], tab[0][toff[g] + b.j]);
+            }
         };
-        rare(std::integral_constant<int, 0>{});
-        if constexpr (G > 1) rare(std::integral_constant<int, 1>{});
-        if constexpr (G > 2) rare(std::integral_constant<int, 2>{});
-        if constexpr (G > 3) rare(std::integral_constant<int, 3>{});
+        chunk_pipeline_1tail<US, SBatch>(
+            n,
+            [&](int j0, SBatch &b) {
+#pragma unroll
+                for (int u = 0; u < US; ++u) sfetch(j0 + u, b.c[u]);
+            },
+            [&](const SBatch &b) {
+#pragma unroll
+                for (int u = 0; u < US; ++u) sstep(b.c[u]);
+            },
+            [&](int j) {
+                SOne b;
+                sfetch(j, b);
+                sstep(b);
+            });
+        base += 64;
+        if (base >= K && p + 1 < npass) {  // the next pass: its channels, the clients again
+            ++p;
+            base = 0;
+            c0 += kSpanMax;
+            pass_rows(p);
+            cr.init(rows, w, K);
+            tab_load(cr.r0, nsz);
+        }
     }
     store_tile<G>(wt, acc, out);
 }

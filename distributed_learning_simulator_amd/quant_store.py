@@ -31,14 +31,18 @@ FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
 # multi-channel tiles (channel rows a multiple of 16): "adaptive" = the widest of
 # 4 / 2 / 1 KiB that spans at most 3 channel rows (4 KiB for rows >= 2048, 2 KiB
 # for rows >= 1024: every lane's channel constants stay in the kernel's staged
-# table), or a fixed width in elements.  The store keeps one table per mode: the
+# table), with rows shorter than ADAPTIVE_MIN_ROW left to the small-tile group (a
+# 1 KiB tile over more than the table's 4 channels is walked once per 4 channels
+# by the FMA lane kernel), or a fixed width in elements.  The store keeps one table per mode: the
 # exact kernel is bound by its instruction count at the clock the chip holds
 #  and runs fastest on 1 KiB tiles (4 waves per SIMD); the FMA mode
 # is bound by the stream and runs fastest on the adaptive ones (same-box A/B,
 # 1000 x ResNet-18: exact 2.01 vs 2.21 ms, FMA 1.96 vs 1.88 ms).
 LANE_TILE = 1024  # the exact mode's (and QuantLayout.tiles()' default)
 LANE_TILE_FMA = "adaptive"
+ADAPTIVE_MIN_ROW = 336  # elements: a 1 KiB lane tile then spans <= 4 channel rows
 F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
+SMALL_TILE = 256  # small int tiles: 64 lanes x 4 elements
 FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
 QALIGN = 256  # bytes: Q tensor starts and row pitch (a 64-B pitch split lines)
 
@@ -122,9 +126,10 @@ class QuantLayout:
           16-element chunk straddles two channels: 3x3 convs, fc layers) are cut
           into LANE_TILE-element tiles from their start, each lane in its own
           channel (adaptive: 4 KiB tiles for rows >= 2048, 2 KiB for rows >= 1024,
-          else 1 KiB: at most 3 channels per tile);
+          1 KiB for rows >= ADAPTIVE_MIN_ROW: at most 4 channels per tile; shorter
+          rows go to the small tiles);
         * fp32 tiles (group 8, <= F32_TILE elements): the fp32 tensors;
-        * small int tiles (group 9, <= F32_TILE elements): the other int tensors
+        * small int tiles (group 9, <= SMALL_TILE elements): the other int tensors
           with rows of at least 4 elements (a lane's 4 span <= 2 channels), except
           their 1 KiB pieces that lie inside one channel (one-channel group 3);
         * general tiles (<= TILE elements): int tensors with rows shorter than 4."""
@@ -143,8 +148,8 @@ class QuantLayout:
                         rows.append((off + e, src + e, min(FAST_TILE, rl - j), kind, cb + c, rl,
                                      j, cend))
                 continue
-            if kind and rl % 16 == 0:
-                lt = LANE_TILE if lane_tile is None else lane_tile
+            lt = LANE_TILE if lane_tile is None else lane_tile
+            if kind and rl % 16 == 0 and (lt != "adaptive" or rl >= ADAPTIVE_MIN_ROW):
                 if lt == "adaptive":
                     lt = 4096 if rl >= 2048 else (2048 if rl >= 1024 else TILE)
                 for e in range(0, n, lt):
@@ -163,8 +168,8 @@ class QuantLayout:
                     if e % rl + ln <= rl:
                         rows.append((off + e, src + e, ln, kind, cb + e // rl, rl, e % rl, cend))
                         continue
-                    for e2 in range(e, e + ln, F32_TILE):
-                        small_rows.append((off + e2, src + e2, min(F32_TILE, e + ln - e2), kind,
+                    for e2 in range(e, e + ln, SMALL_TILE):
+                        small_rows.append((off + e2, src + e2, min(SMALL_TILE, e + ln - e2), kind,
                                            cb + e2 // rl, rl, e2 % rl, cend))
                 continue
             for e in range(0, n, TILE):

@@ -548,6 +548,62 @@ def test_dequant_fedavg_lane_tiles_resnet_shapes(K):
                 assert err <= 1e-6, (name, err)
 
 
+def test_dequant_fedavg_fma_lane_tiles_multipass(monkeypatch):
+    """FMA-mode lane tiles over more channels than the kernel's staged table (4):
+    1 KiB lane tiles on rows of 16, 48 and 64 elements (up to 64 channels per
+    tile, walked in passes of 4 channels while the other lanes read the table's
+    zero row), int8 symmetric and uint8 with zero points, K across two 64-client
+    chunks; every tensor within the north-star 1e-6 normwise of the exact
+    oracle.  The adaptive table never builds such tiles (rows < 336 go to the
+    small-tile group); a caller's fixed-width table may."""
+    from distributed_learning_simulator_amd import _native, quant_store as qs
+    from distributed_learning_simulator_amd.quant_store import QTILE_DTYPE, QuantizedClientStore
+    monkeypatch.setattr(qs, "LANE_TILE_FMA", 1024)
+    K = 70
+    g = torch.Generator().manual_seed(29)
+    shapes = {"pw16": (64, 16, 1, 1), "pw48": (40, 48, 1, 1), "pw64": (32, 64, 1, 1)}
+    payloads, n = [], []
+    for _ in range(K):
+        p = {}
+        for name, s in shapes.items():
+            C = s[0]
+            if name == "pw48":  # uint8 with zero points
+                p[name] = (torch.randint(0, 256, s, generator=g, dtype=torch.uint8),
+                           torch.rand(C, generator=g, dtype=torch.float64) * 1e-3 + 1e-5,
+                           torch.randint(0, 256, (C,), generator=g))
+            else:
+                p[name] = (torch.randint(-128, 128, s, generator=g, dtype=torch.int8),
+                           torch.rand(C, generator=g, dtype=torch.float64) * 1e-2 + 1e-4,
+                           torch.zeros(C, dtype=torch.int64))
+        payloads.append(p)
+        n.append(int(torch.randint(1, 1000, (1,), generator=g)))
+    store = QuantizedClientStore(payloads[0], dev, capacity=K)
+    t = store.tiles_fma.cpu().numpy().view(QTILE_DTYPE)
+    lanes = t[sum(store.nfast_fma[:4]):sum(store.nfast_fma[:8])]
+    span = (lanes["row_pos"] + lanes["len"] - 1) // lanes["row_len"] + 1
+    assert len(lanes) > 0 and span.max() > 4  # multi-pass tiles are used
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    order = list(torch.randperm(K, generator=g).tolist())
+    layout = [(k, tuple(v[0].shape)) for k, v in payloads[0].items()]
+    clients = [{k: tuple(t.numpy() for t in v) for k, v in p.items()} for p in payloads]
+    ref = oquant.dequant_fedavg(clients, n, order, layout)
+    full = torch.full((store.layout.P,), float("nan"), device=dev)
+    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order],
+                                          out=full, mode=_native.FEDAVG_FMA))
+    assert_padding_zero(store.layout, full)
+    off = 0
+    for name, shape in layout:
+        m = int(np.prod(shape))
+        got, want = out[name].reshape(-1).cpu().numpy(), ref[off:off + m]
+        off += m
+        err = np.linalg.norm(got.astype(np.float64) - want) / np.linalg.norm(want)
+        assert err <= 1e-6, (name, err)
+
+
 def test_qat_weight_fake_quant_ste():
     """The fed_quant worker's quantization-aware training (ref
     workers/fed_quant_worker.py:19-20): conv / linear weights enter the forward

@@ -71,13 +71,14 @@ def test_quant_layout_channel_aligned_tiles(lane_tile, monkeypatch):
     """Long channel rows (multiple of 64, last 1 KiB slice at least 7/8 full) get
     channel-aligned tiles of up to 4096 elements, grouped by slice count; other
     int tensors with rows a multiple of 16 get multi-channel (lane) tiles from their
-    start: LANE_TILE elements, or adaptive (4 KiB for rows >= 2048: conv and mid)."""
+    start: LANE_TILE elements, or adaptive (4 KiB for rows >= 2048: conv and mid;
+    rows < ADAPTIVE_MIN_ROW, pw's 64, go to the small tiles)."""
     from distributed_learning_simulator_amd import quant_store
     from distributed_learning_simulator_amd.quant_store import QuantLayout
     monkeypatch.setattr(quant_store, "LANE_TILE", lane_tile)
     LANE_TILE = 4096 if lane_tile == "adaptive" else lane_tile
     shapes = {"fc": (3, 25088), "conv": (2, 512, 3, 3), "mid": (4, 256, 3, 3), "k": (2, 1024),
-              "c1": (5, 3, 3, 3)}
+              "c1": (5, 3, 3, 3), "pw": (8, 64, 1, 1)}
     payload = {k: (torch.zeros(s, dtype=torch.int8), torch.ones(s[0]), torch.zeros(s[0]))
                for k, s in shapes.items()}
     ql = QuantLayout(payload)
@@ -85,15 +86,16 @@ def test_quant_layout_channel_aligned_tiles(lane_tile, monkeypatch):
     # fc: 6 x 4096 + 512 per channel (2 % idle lanes); k: 1024; conv (row 4608:
     # 11 % idle lanes in its last slice) and mid (row 2304): lane tiles of
     # LANE_TILE from their start; c1 (row 27): general 1 KiB tiles
-    if lane_tile == 1024:
-        assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 0, 0, 0, 9 + 9) and nfast[8] == 0
+    if lane_tile == 1024:  # pw: one 512-element lane tile over 8 channel rows
+        assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 0, 0, 0, 9 + 9 + 1) and nfast[8] == 0
+        assert nfast[9] == (5 * 27 + 255) // 256  # c1 (rows of 27): small tiles
     else:  # 9216-element tensors: 4096 + 4096 + 1024
         assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 2 + 2, 0, 0, 1 + 1) and nfast[8] == 0
         lanes = t[sum(nfast[:4]):sum(nfast[:8])]
-        # at most 3 channel rows per lane tile (the kernel's staged table holds 4)
+        # at most 4 channel rows per lane tile (the FMA kernel's staged table)
         assert max((int(r["row_pos"]) + int(r["len"]) - 1) // int(r["row_len"]) + 1
-                   for r in lanes) <= 3
-    assert nfast[9] == (5 * 27 + 255) // 256  # c1 (rows of 27): small tiles
+                   for r in lanes) <= 4
+        assert nfast[9] == (5 * 27 + 255) // 256 + 512 // 256  # c1 and pw: small tiles
     nf = sum(nfast)
     one = t[:sum(nfast[:4])]
     sl = [(int(r["len"]) + 1023) // 1024 for r in one]

@@ -180,10 +180,14 @@ def setup(dev, want=()):
             + 4 * sr.layout.numel
         saved = qs.LANE_TILE
 
-        def table(lane_tile):
+        def table(lane_tile, f32_tile=None, small_tile=None):
+            keep = (qs.F32_TILE, qs.SMALL_TILE)
             qs.LANE_TILE = lane_tile
+            qs.F32_TILE = f32_tile or keep[0]
+            qs.SMALL_TILE = small_tile or keep[1]
             tt, nft = qlr.tiles()
             qs.LANE_TILE = saved
+            qs.F32_TILE, qs.SMALL_TILE = keep
             return torch.from_numpy(tt.view(np.uint8).copy()).to(dev), tt, nft
 
         def qmode(tab, rows_t, w_t, tot, mode):
@@ -200,6 +204,12 @@ def setup(dev, want=()):
         W["quant_r18_a"] = (qmode(tab_a, r1k, w1k, t1k, 0), nb, qo18)
         # DLS_FEDAVG_FMA (1e-6 tolerance mode) on the same 1000 clients
         W["quant_r18_fma"] = (qmode(tab_f, r1k, w1k, t1k, 1), nb, qo18)
+        # smaller fp32 / small-int tiles: more side-stream waves (latency-bound groups)
+        for ft, stl in ((64, None), (64, 64), (128, 128)):
+            tag = f"_f{ft}" + (f"s{stl}" if stl else "")
+            W["quant_r18_fma" + tag] = (
+                qmode(table(qs.LANE_TILE_FMA, ft, stl), r1k, w1k, t1k, 1), nb, qo18)
+            W["quant_r18" + tag] = (qmode(table(saved, ft, stl), r1k, w1k, t1k, 0), nb, qo18)
         W["quant_r18_l1_fma"] = (qmode(tab_1, r1k, w1k, t1k, 1), nb, qo18)
         W["quant_r18_a_fma"] = (qmode(tab_a, r1k, w1k, t1k, 1), nb, qo18)
         # >= 10 ms dispatches for clock / counter probes: the 1000 client rows walked
