@@ -690,20 +690,29 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     hand-written pass, logits bit-identical to the module's forward), again with the
     module's own forward (``fused_eval=False``: MIOpen batch norm, separate add and
     ReLU kernels), and with non-deterministic convolutions (the cost of determinism)."""
+    ts = time.perf_counter()
     server = _shapley_eval_server(args, dev)
+    if rank == 0:
+        log(f"shapley_evals: server and test set ready in {time.perf_counter() - ts:.1f} s")
     coal = _shapley_coalitions(50, (args.evals + 2) * world, SEED + 7)
 
     def timed(fused, deterministic=True):
         server.tester.fused_eval = fused
         server.tester.deterministic = deterministic
+        tw = time.perf_counter()
         server.evaluate_subsets(coal[: 2 * world])  # MIOpen kernel selection, warm caches
         torch.cuda.synchronize()
+        if rank == 0:
+            log(f"shapley_evals: warm-up (fused={fused}, deterministic={deterministic}) "
+                f"{time.perf_counter() - tw:.1f} s")
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         vals = server.evaluate_subsets(coal[2 * world:])
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        if rank == 0:
+            log(f"shapley_evals: {len(coal) - 2 * world} evals in {el:.1f} s")
         if world > 1:
             el = _max_over_ranks(el, dev)
         return el, vals
@@ -720,7 +729,8 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     bn = bench_bn_act(args, dev) if rank == 0 else None
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
-                      f"{args.eval_images} CIFAR-10-shaped images (fp32, NHWC, batch 1000)",
+                      f"{args.eval_images} CIFAR-10-shaped images (fp32, batch 1000, NCHW: "
+                      f"MIOpen's deterministic convolutions)",
             "value": round(n / el, 3), "unit": "subset-evals/s (all GPUs)",
             "ms_per_eval_per_gpu": round(el / n * world * 1e3, 2),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
@@ -728,8 +738,8 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
             "nondeterministic_convs": {"value": round(n / el_nd, 3),
                                        "unit": "subset-evals/s (all GPUs)",
                                        "note": "the same path with MIOpen's default (not "
-                                               "run-to-run reproducible) convolution algorithms: "
-                                               "what determinism costs"},
+                                               "run-to-run reproducible) convolution algorithms "
+                                               "on NHWC activations: what determinism costs"},
             "module_forward": {"value": round(n / el_m, 3), "unit": "subset-evals/s (all GPUs)",
                                "ms_per_eval_per_gpu": round(el_m / n * world * 1e3, 2),
                                "max_utility_diff": round(

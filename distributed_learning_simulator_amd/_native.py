@@ -76,6 +76,7 @@ SIGNATURES = {
     "dls_bn_act_nhwc_f32": ([_p, _i64, _i32, _p, _p, _p, _i32, _p, _p], _i32),
     "dls_bn_fold_exact_f32": ([_p, _p, _p, _p, _f32, _i32, _p, _p], _i32),
     "dls_bn_act_exact_nhwc_f32": ([_p, _i64, _i32, _p, _p, _i32, _p, _p], _i32),
+    "dls_bn_act_exact_nchw_f32": ([_p, _i64, _i32, _i64, _p, _p, _i32, _p, _p], _i32),
 }
 
 _lib = None
@@ -329,3 +330,25 @@ def bn_act_exact_nhwc(x, consts, residual=None, relu=True, out=None, inplace=Fal
                                            int(bool(relu)), _ptr(out),
                                            _stream(stream, x)), "dls_bn_act_exact_nhwc_f32")
     return out
+
+
+def bn_act_exact_nchw(x, consts, residual=None, relu=True, out=None, inplace=False, stream=None):
+    """bn_act_exact_nhwc over an NCHW-contiguous [N, C, H, W] fp32 activation
+    (dls_bn_act_exact_nchw_f32; H*W a multiple of 4)."""
+    N, C, H, W = x.shape
+    if not x.is_contiguous() or (residual is not None and not residual.is_contiguous()):
+        raise RuntimeError("bn_act_exact_nchw: activations must be NCHW contiguous")
+    if out is None:
+        out = x if inplace else torch.empty_like(x, memory_format=torch.contiguous_format)
+    _check(lib().dls_bn_act_exact_nchw_f32(_ptr(x), N, C, H * W, _ptr(consts), _ptr(residual),
+                                           int(bool(relu)), _ptr(out),
+                                           _stream(stream, x)), "dls_bn_act_exact_nchw_f32")
+    return out
+
+
+def bn_act_exact(x, consts, residual=None, relu=True, out=None, inplace=False, stream=None):
+    """The exact eval batch-norm pass in the activation's own layout: channels_last
+    (NHWC) or contiguous (NCHW)."""
+    if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        return bn_act_exact_nhwc(x, consts, residual, relu, out, inplace, stream)
+    return bn_act_exact_nchw(x, consts, residual, relu, out, inplace, stream)

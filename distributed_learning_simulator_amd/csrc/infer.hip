@@ -154,10 +154,101 @@ __global__ __launch_bounds__(kBnBlock) void k_bn_act_exact(const f32x4 *x, int64
     }
 }
 
+// The same pass over NCHW (contiguous) activations: a float4 holds 4 spatial
+// positions of one (image, channel) plane (HW % 4 == 0), whose channel is
+// (k / HW4) % C; shifts and masks when HW4 and C are powers of two.  MIOpen's
+// deterministic convolutions exist for NCHW only (its NHWC ones fall back to a
+// naive kernel, ~100x slower: profiles/r04q_eval_det.txt), so the Inferencer's
+// reproducible path runs NCHW.
+template <bool POW2, bool RES, bool RELU>
+__global__ __launch_bounds__(kBnBlock) void k_bn_act_exact_nchw(const f32x4 *x, int64_t n4, int C,
+                                                                int HW4, int sh, int cm,
+                                                                const float *__restrict__ consts,
+                                                                const f32x4 *r, f32x4 *y) {
+    const int64_t stride = (int64_t)gridDim.x * kBnBlock;
+    int64_t i = (int64_t)blockIdx.x * kBnBlock + threadIdx.x;
+    auto one = [&](f32x4 v, f32x4 rv, int64_t k) {
+        const int c = POW2 ? (int)((k >> sh) & cm) : (int)((k / HW4) % C);
+        const float m = consts[c], iv = consts[C + c], wv = consts[2 * C + c],
+                    bv = consts[3 * C + c];
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float h = (v[e] - m) * iv;
+            float t = __builtin_fmaf(wv, h, bv);
+            if (RES) t = t + rv[e];
+            if (RELU) t = t > 0.f ? t : (t == t ? 0.f : t);  // relu keeps NaN, as torch
+            o[e] = t;
+        }
+        return o;
+    };
+    for (; i + (kBnUnroll - 1) * stride < n4; i += kBnUnroll * stride) {
+        f32x4 v[kBnUnroll], rv[kBnUnroll];
+#pragma unroll
+        for (int u = 0; u < kBnUnroll; ++u) {
+            v[u] = __builtin_nontemporal_load(x + i + u * stride);
+            if (RES) rv[u] = __builtin_nontemporal_load(r + i + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < kBnUnroll; ++u)
+            y[i + u * stride] = one(v[u], RES ? rv[u] : f32x4{}, i + u * stride);
+    }
+    for (; i < n4; i += stride) {
+        const f32x4 v = x[i];
+        y[i] = one(v, RES ? r[i] : f32x4{}, i);
+    }
+}
+
 }  // namespace
 }  // namespace dls
 
 using namespace dls;
+
+extern "C" int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
+                                         const float *consts, const float *residual, int32_t relu,
+                                         float *y, dls_stream_t stream) {
+    DLS_REQUIRE(x && consts && y, DLS_EINVAL, "dls_bn_act_exact_nchw_f32: null pointer");
+    DLS_REQUIRE(N > 0 && C > 0 && HW > 0 && HW % 4 == 0 && HW / 4 < (1 << 30), DLS_EINVAL,
+                "dls_bn_act_exact_nchw_f32: N=%lld C=%d HW=%lld (HW a multiple of 4)",
+                (long long)N, C, (long long)HW);
+    DLS_REQUIRE(aligned16(x) && aligned16(y) && (!residual || aligned16(residual)), DLS_ELAYOUT,
+                "dls_bn_act_exact_nchw_f32: 16-byte alignment");
+    const int64_t n4 = N * C * (HW / 4);
+    const int HW4 = (int)(HW / 4);
+    int64_t blocks = (n4 + (int64_t)kBnBlock * kBnUnroll - 1) / ((int64_t)kBnBlock * kBnUnroll);
+    const int64_t cap = (int64_t)resident_blocks(reinterpret_cast<const void *>(
+                                                     k_bn_act_exact_nchw<true, false, true>),
+                                                 kBnBlock, 0) * 4;
+    if (blocks > cap) blocks = cap;
+    if (blocks < 1) blocks = 1;
+    const bool pow2 = (HW4 & (HW4 - 1)) == 0 && (C & (C - 1)) == 0;
+    int sh = 0;
+    while ((1 << sh) < HW4) ++sh;
+    const f32x4 *xv = reinterpret_cast<const f32x4 *>(x);
+    const f32x4 *rv = reinterpret_cast<const f32x4 *>(residual);
+    f32x4 *yv = reinterpret_cast<f32x4 *>(y);
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)blocks), block(kBnBlock);
+    const bool res = residual != nullptr;
+#define DLS_BNC(P_, R_, A_)                                                                    \
+    hipLaunchKernelGGL((k_bn_act_exact_nchw<P_, R_, A_>), grid, block, 0, st, xv, n4, (int)C, \
+                       HW4, sh, (int)C - 1, consts, rv, yv)
+    if (pow2) {
+        if (res) {
+            if (relu) DLS_BNC(true, true, true); else DLS_BNC(true, true, false);
+        } else {
+            if (relu) DLS_BNC(true, false, true); else DLS_BNC(true, false, false);
+        }
+    } else {
+        if (res) {
+            if (relu) DLS_BNC(false, true, true); else DLS_BNC(false, true, false);
+        } else {
+            if (relu) DLS_BNC(false, false, true); else DLS_BNC(false, false, false);
+        }
+    }
+#undef DLS_BNC
+    return check_launch("dls_bn_act_exact_nchw_f32");
+}
 
 extern "C" int dls_bn_fold_exact_f32(const float *weight, const float *bias, const float *mean,
                                      const float *var, float eps, int32_t C, float *consts,

@@ -43,19 +43,19 @@ class _Block(nn.Module):
         return F.relu(out + self.shortcut(x))
 
     def forward_fused(self, x, fold):
-        """Eval-mode forward on channels_last activations: each batch norm (with the
-        ReLU / residual add after it) is one dls_bn_act_exact_nhwc_f32 pass, in
+        """Eval-mode forward: each batch norm (with the ReLU / residual add after it)
+        is one dls_bn_act_exact_{nhwc,nchw}_f32 pass (the activation's layout), in
         place on the convolution's output; the same ops and roundings as forward()
         on the GPU, so the same bits."""
         from . import _native
-        out = _native.bn_act_exact_nhwc(self.conv1(x), fold[id(self.bn1)], relu=True, inplace=True)
+        out = _native.bn_act_exact(self.conv1(x), fold[id(self.bn1)], relu=True, inplace=True)
         out = self.conv2(out)
         if len(self.shortcut):
-            sc = _native.bn_act_exact_nhwc(self.shortcut[0](x), fold[id(self.shortcut[1])],
+            sc = _native.bn_act_exact(self.shortcut[0](x), fold[id(self.shortcut[1])],
                                            relu=False, inplace=True)
         else:
             sc = x
-        return _native.bn_act_exact_nhwc(out, fold[id(self.bn2)], residual=sc, relu=True,
+        return _native.bn_act_exact(out, fold[id(self.bn2)], residual=sc, relu=True,
                                          inplace=True)
 
 
@@ -98,13 +98,13 @@ class ResNet18(nn.Module):
         return fold
 
     def forward_fused(self, x, fold):
-        """forward() for utility evaluation on the GPU: channels_last activations,
+        """forward() for utility evaluation on the GPU: NHWC or NCHW activations,
         MIOpen convolutions, every batch norm + ReLU (+ residual add) fused into one
-        hand-written pass (dls_bn_act_exact_nhwc_f32) with the batch-norm library's
-        own arithmetic: the logits are bit-identical to forward()'s
-        (tests/test_gpu_infer.py)."""
+        hand-written pass (dls_bn_act_exact_nhwc_f32 / _nchw_f32) with the
+        batch-norm library's own arithmetic: the logits are bit-identical to
+        forward()'s (tests/test_gpu_infer.py)."""
         from . import _native
-        out = _native.bn_act_exact_nhwc(self.conv1(x), fold[id(self.bn1)], relu=True, inplace=True)
+        out = _native.bn_act_exact(self.conv1(x), fold[id(self.bn1)], relu=True, inplace=True)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 out = blk.forward_fused(out, fold)

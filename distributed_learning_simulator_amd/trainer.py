@@ -86,7 +86,11 @@ class Inferencer:
     convolution solutions.  Those are torch's process-wide switches, set for the
     duration of ``inference()`` / ``logits()`` and restored after it (worker
     threads that train meanwhile also get deterministic convolutions; their
-    results stay correct).
+    results stay correct).  MIOpen's deterministic solutions are NCHW ones: on
+    channels_last activations it falls back to a naive kernel (~19 s instead of
+    0.2 s per 10k CIFAR images, profiles/r04q_eval_det.txt), so the reproducible
+    path keeps activations NCHW; ``deterministic=False`` runs channels_last
+    (NHWC), the faster layout for MIOpen's default algorithms.
 
     Models that have a ``forward_fused`` eval path (models.ResNet18) run it on the
     GPU (``fused_eval``, default on): every batch norm + ReLU (+ residual add) as
@@ -108,7 +112,7 @@ class Inferencer:
         self.device = device or next(model.parameters()).device
         self.accuracy_metric = _Accuracy()
         self.loss_metric = _Loss()
-        self._fused_checked = None  # None: not yet checked; else the check's verdict
+        self._fused_checked = None  # None: not yet checked; else (layout, the check's verdict)
 
     def set_device(self, device):
         self.device = torch.device(device)
@@ -119,19 +123,24 @@ class Inferencer:
             return contextlib.nullcontext()
         return _deterministic_convs()
 
+    def _memory_format(self):
+        """The activation layout of the GPU forward: NCHW with deterministic
+        convolutions (MIOpen has no fast deterministic NHWC ones), else NHWC."""
+        return torch.contiguous_format if self.deterministic else torch.channels_last
+
     def _fused_matches_module(self):
         """One eval batch norm of the model through the fused pass vs ``bn(x)`` on a
-        small channels_last activation: True when the bits agree."""
+        small activation in the forward's layout: True when the bits agree."""
         from . import _native
         bn = next((m for m in self.model.modules() if isinstance(m, torch.nn.BatchNorm2d)), None)
         if bn is None:
             return True
         g = torch.Generator().manual_seed(0)
-        x = (torch.randn(2, bn.num_features, 5, 5, generator=g) * 3).to(self.device)
-        x = x.contiguous(memory_format=torch.channels_last)
+        x = (torch.randn(2, bn.num_features, 6, 6, generator=g) * 3).to(self.device)
+        x = x.contiguous(memory_format=self._memory_format())
         consts = torch.empty(4 * bn.num_features, device=self.device)
         _native.bn_fold_exact(bn, consts)
-        y = _native.bn_act_exact_nhwc(x, consts, relu=False)
+        y = _native.bn_act_exact(x, consts, relu=False)
         return torch.equal(y.view(torch.int32), bn(x).view(torch.int32))
 
     def _fused_forward(self, X):
@@ -140,23 +149,26 @@ class Inferencer:
         fused = getattr(self.model, "forward_fused", None)
         if fused is None:
             return None
-        if self._fused_checked is None:
-            self._fused_checked = self._fused_matches_module()
-            if not self._fused_checked:
+        fmt = self._memory_format()
+        if self._fused_checked is None or self._fused_checked[0] != fmt:
+            self._fused_checked = (fmt, self._fused_matches_module())
+            if not self._fused_checked[1]:
                 import logging
                 logging.getLogger("distributed_learning_simulator_amd").warning(
                     "fused eval batch norm differs from the module's on this stack; "
                     "running the module's forward")
-        return fused if self._fused_checked else None
+        return fused if self._fused_checked[1] else None
 
     def _batches(self):
         """Logits of every batch, in order (the model in eval mode)."""
         X, y = self.dataset
         self.model.eval()
+        fmt = self._memory_format()
         if X.dim() == 4 and torch.device(self.device).type == "cuda":
             # NHWC convolutions: measured 8-18 % faster than NCHW for this model family
-            # on MI355X (tools/eval_probe.py); results are the same up to fp32 reassociation
-            self.model.to(memory_format=torch.channels_last)
+            # on MI355X with MIOpen's default algorithms (tools/eval_probe.py); the
+            # deterministic ones are NCHW (tools/eval_det_probe.py)
+            self.model.to(memory_format=fmt)
         # a model with a fused eval forward (models.ResNet18): every batch norm + ReLU
         # (+ residual add) is one hand-written NHWC pass instead of three kernels
         fused = self._fused_forward(X)
@@ -165,7 +177,7 @@ class Inferencer:
             xb = X[i:i + self.batch_size].to(self.device, non_blocking=True)
             yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
             if xb.dim() == 4 and xb.is_cuda:
-                xb = xb.contiguous(memory_format=torch.channels_last)
+                xb = xb.contiguous(memory_format=fmt)
             yield (fused(xb, fold) if fused is not None else self.model(xb)), yb
 
     @torch.no_grad()

@@ -267,6 +267,12 @@ int dls_bn_fold_exact_f32(const float *weight, const float *bias, const float *m
                           dls_stream_t stream);
 int dls_bn_act_exact_nhwc_f32(const float *x, int64_t rows, int32_t C, const float *consts,
                               const float *residual, int32_t relu, float *y, dls_stream_t stream);
+/* The same exact pass over an NCHW (contiguous) [N, C, H, W] fp32 tensor, HW =
+ * H*W a multiple of 4 (MIOpen's deterministic convolutions are NCHW ones: the
+ * reproducible utility evaluation runs in that layout).  y may alias x. */
+int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
+                              const float *consts, const float *residual, int32_t relu, float *y,
+                              dls_stream_t stream);
 
 #ifdef __cplusplus
 }

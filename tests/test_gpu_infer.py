@@ -5,7 +5,7 @@ servers/fed_server.py:26-32) with its hand-written eval batch norm.
   torch (alpha = 1/sqrt(var+eps) * w, beta = b - mean * alpha, y = x*alpha + beta,
   + residual, ReLU): bit-exact, every flag combination, ragged sizes, C not a
   divisor of the grid (the per-iteration channel path), in place.
-* dls_bn_fold_exact_f32 / dls_bn_act_exact_nhwc_f32 against torch's own eval
+* dls_bn_fold_exact_f32 / dls_bn_act_exact_{nhwc,nchw}_f32 against torch's own eval
   BatchNorm2d on the GPU (MIOpen's inference kernel), + residual, ReLU: bit-exact.
 * ResNet-18 forward_fused (the exact pass) vs torch's own eval forward: logits
   bit-identical with MIOpen's deterministic convolutions (its default kernels for
@@ -13,6 +13,8 @@ servers/fed_server.py:26-32) with its hand-written eval batch norm.
   Inferencer's accuracy and loss equal on both paths.
   Utility parity with the reference's tester is unpinned (its library is absent).
 """
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -107,6 +109,41 @@ def test_bn_act_exact_matches_torch_eval(N, C, H, W, res, relu):
     assert torch.equal(y2[m].view(torch.int32), ref[m].view(torch.int32))
 
 
+@pytest.mark.parametrize("N,C,H,W", [(64, 64, 32, 32), (16, 128, 16, 16), (7, 512, 4, 4),
+                                     (3, 12, 5, 4), (2, 96, 2, 6)])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_bn_act_exact_nchw_matches_torch_eval(N, C, H, W, res, relu):
+    """The exact pass over NCHW-contiguous activations (dls_bn_act_exact_nchw_f32,
+    the deterministic utility path's layout) = torch's eval BatchNorm2d (+ residual
+    add, ReLU) bit for bit, NaN kept, in place; channel counts and planes that are
+    and are not powers of two."""
+    from distributed_learning_simulator_amd import _native
+    g = torch.Generator().manual_seed(N + 3 * C + H)
+    bn = _bn(C, g)
+    with torch.no_grad():
+        bn.running_var[0] = 1e-3
+    consts = torch.empty(4 * C, device=dev)
+    _native.bn_fold_exact(bn, consts)
+    x = (torch.randn(N, C, H, W, generator=g) * 3).to(dev)
+    x[0, 0, 0, 0] = float("nan")
+    r = torch.randn(N, C, H, W, generator=g).to(dev) if res else None
+    with torch.no_grad():
+        ref = bn(x)
+        if res:
+            ref = ref + r
+        if relu:
+            ref = torch.relu(ref)
+    y = _native.bn_act_exact(x, consts, residual=r, relu=relu)
+    assert y.is_contiguous()
+    assert torch.isnan(y[0, 0, 0, 0]) and torch.isnan(ref[0, 0, 0, 0])
+    m = ~torch.isnan(ref)
+    assert torch.equal(y[m].view(torch.int32), ref[m].view(torch.int32))
+    y2 = _native.bn_act_exact_nchw(x.clone(), consts, residual=r, relu=relu, inplace=True)
+    assert torch.equal(y2[m].view(torch.int32), ref[m].view(torch.int32))
+    with pytest.raises(RuntimeError):  # a channels_last activation is not NCHW
+        _native.bn_act_exact_nchw(x.contiguous(memory_format=torch.channels_last), consts)
+
+
 @pytest.fixture
 def deterministic_convs():
     """MIOpen's convolutions for ResNet-18's 512-channel layer pick a kernel whose
@@ -119,7 +156,8 @@ def deterministic_convs():
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
 
 
-def test_resnet18_fused_eval_matches_torch(deterministic_convs):
+@pytest.mark.parametrize("fmt", ["nhwc", "nchw"])
+def test_resnet18_fused_eval_matches_torch(deterministic_convs, fmt):
     from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
     from distributed_learning_simulator_amd.trainer import Inferencer
     torch.manual_seed(0)
@@ -133,8 +171,13 @@ def test_resnet18_fused_eval_matches_torch(deterministic_convs):
                 m.weight.copy_(torch.rand(m.num_features, generator=g) + 0.5)
                 m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
     X, y = synthetic_classification(600, (3, 32, 32), seed=3)
-    model.eval().to(memory_format=torch.channels_last)
-    xb = X.to(dev).contiguous(memory_format=torch.channels_last)
+    mf = torch.channels_last if fmt == "nhwc" else torch.contiguous_format
+    model.eval().to(memory_format=mf)
+    xb = X.to(dev).contiguous(memory_format=mf)
+    if fmt == "nhwc":  # MIOpen's deterministic NHWC convolutions are its naive kernels
+        xb = xb[:64]
+        y = y[:64]
+        X = X[:64]
     with torch.no_grad():
         ref = model(xb)
         assert torch.equal(model(xb).view(torch.int32), ref.view(torch.int32))  # a function
@@ -145,13 +188,14 @@ def test_resnet18_fused_eval_matches_torch(deterministic_convs):
     # forward over the same batches (MIOpen may pick other algorithms for other
     # batch sizes)
     inf = Inferencer(model, (X, y), batch_size=256, device=dev)
-    assert inf.fused_eval is True
+    assert inf.fused_eval is True and inf.deterministic  # the NCHW path
     loss, acc, _ = inf.inference()
     plain = Inferencer(model, (X, y), batch_size=256, device=dev, fused_eval=False)
     loss0, acc0, _ = plain.inference()
     assert acc == acc0 and float(loss) == float(loss0)
+    xq = X.to(dev)  # the Inferencer's deterministic layout: NCHW
     with torch.no_grad():
-        pred = torch.cat([model(xb[i:i + 256]).argmax(1) for i in range(0, xb.shape[0], 256)])
+        pred = torch.cat([model(xq[i:i + 256]).argmax(1) for i in range(0, xq.shape[0], 256)])
     assert acc0 == int((pred.cpu() == y).sum()) / y.numel()  # the Inferencer's int / n
     assert np.isfinite(float(loss))
 
@@ -160,7 +204,9 @@ def test_utility_is_a_function_of_the_model():
     """the product's default tester (no fixture, default flags)
     gives bit-identical logits and the same accuracy / loss for the same model on
     repeated evaluations and on fresh Inferencers, at ResNet-18 x 10k CIFAR-shaped
-    images (the config-5 utility), and leaves torch's global flags as it found them."""
+    images (the config-5 utility), and leaves torch's global flags as it found them.
+    And it stays fast: MIOpen's deterministic NHWC convolutions are naive kernels
+    (19 s per evaluation, profiles/r04q_eval_det.txt), the NCHW path ~0.2 s."""
     from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
     from distributed_learning_simulator_amd.trainer import Inferencer
     torch.manual_seed(7)
@@ -175,8 +221,11 @@ def test_utility_is_a_function_of_the_model():
     assert (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark) == flags
     b = Inferencer(model, (X, y), device=dev)
     lb = b.logits()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     loss_b, acc_b, _ = b.inference()
-    assert a._fused_checked is True  # the fused pass matched bn(x) on this stack
+    assert time.perf_counter() - t0 < 3.0  # not MIOpen's naive-kernel fallback
+    assert a._fused_checked == (torch.contiguous_format, True)  # fused pass == bn(x) here
     assert torch.equal(la.view(torch.int32), la2.view(torch.int32))
     assert torch.equal(la.view(torch.int32), lb.view(torch.int32))
     assert acc_a == acc_b and float(loss_a) == float(loss_b)
