@@ -276,6 +276,13 @@ __device__ __forceinline__ void accum16_fma(float (&acc)[16], u32x4 qv, f32x2 cz
 // once per chunk and channel)
 __device__ __forceinline__ float fma_coef(float s, float wk, float N) { return (s * wk) / N; }
 
+// FMA mode: every lane-tile width in one launch (k_dequant_lanes_fma_any); 0: one
+// launch per width, the narrower ones on side streams (A/B knob)
+#ifndef DLS_QUANT_FMA_ANY
+#define DLS_QUANT_FMA_ANY 1
+#endif
+constexpr bool kQuantFmaAny = DLS_QUANT_FMA_ANY != 0;
+
 #ifndef DLS_QUANT_PROBE
 #define DLS_QUANT_PROBE 0  // 1: stream-only timing probe (loads + a xor per dword; wrong output)
 // 2: as 1, and lane_tile skips its per-chunk scale staging (no sz gathers, LDS table, ballot)
@@ -615,9 +622,9 @@ __device__ __forceinline__ void store16(const WaveTile &wt, float (&acc)[16],
         o[v] = f32x4{acc[4 * v], acc[4 * v + 1], acc[4 * v + 2], acc[4 * v + 3]};
 }
 
-template <int G>
+template <int G, bool EXT = false>
 __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][16],
-                                           float *__restrict__ out);
+                                           float *__restrict__ out, float *mine = nullptr);
 
 // One-channel tiles of up to 4 KiB: slice g of the tile is lanes'
 // 16-element chunks 1024 g + 16 lane; the wave walks the clients once for all
@@ -819,11 +826,15 @@ __device__ __forceinline__ void lane_tile(const WaveTile &wt, const uint8_t *__r
 
 // Write a wave tile's G slices of accumulators, transposed through LDS so that
 // each store instruction writes 1 KiB contiguous.
-template <int G>
+// EXT: mine is the wave's 4 KiB of LDS from the caller (a kernel running several
+// tile widths holds ONE buffer); else the function's own
+template <int G, bool EXT>
 __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][16],
-                                           float *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
-    float *mine = xs[threadIdx.x >> 6];
+                                           float *__restrict__ out, float *mine) {
+    if constexpr (!EXT) {
+        __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
+        mine = xs[threadIdx.x >> 6];
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         const int e0 = 1024 * g + 16 * __lane_id();
@@ -981,14 +992,17 @@ __device__ __forceinline__ void fma_one_channel_tile(const WaveTile &wt, const u
 // one piece).  The zero point is always subtracted: x + (-z) is exact and
 // x + (-0) == x, so a chunk of zero points 0 gives the bits of the
 // subtraction-free form.
-template <bool SIGNED, int G>
+template <bool SIGNED, int G, bool EXT = false>
 __device__ __forceinline__ void fma_lane_tile(const WaveTile &wt, const uint8_t *__restrict__ Q,
                                               int64_t ldq, const f32x2 *__restrict__ sz, SzLayout L,
                                               const int32_t *__restrict__ rows,
                                               const float *__restrict__ w, int K, float N,
-                                              float *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) f32x2 ftab[kBlock / 64][kSpanMax + 1][64];
-    f32x2(*tab)[64] = ftab[threadIdx.x >> 6];
+                                              float *__restrict__ out,
+                                              f32x2 (*tab)[64] = nullptr, float *xsw = nullptr) {
+    if constexpr (!EXT) {  // else the caller's (k_dequant_lanes_fma_any)
+        __shared__ __attribute__((aligned(16))) f32x2 ftab[kBlock / 64][kSpanMax + 1][64];
+        tab = ftab[threadIdx.x >> 6];
+    }
     tab[kSpanMax][__lane_id()] = f32x2{0.f, 0.f};  // the zero row
     float acc[G][16];
     uint32_t qoff[G];
@@ -1087,7 +1101,7 @@ __device__ __forceinline__ void fma_lane_tile(const WaveTile &wt, const uint8_t 
             tab_load(cr.r0, nsz);
         }
     }
-    store_tile<G>(wt, acc, out);
+    store_tile<G, EXT>(wt, acc, out, xsw);
 }
 
 template <int G>
@@ -1114,6 +1128,43 @@ __global__ __launch_bounds__(kBlock) void k_dequant_lanes_fma(
         fma_lane_tile<true, G>(wt, Q, ldq, sz, L, rows, w, K, d.b, out);
     else
         fma_lane_tile<false, G>(wt, Q, ldq, sz, L, rows, w, K, d.b, out);
+}
+
+// Every lane-tile group (4, 3, 2 and 1 KiB tiles, the table's groups 4-7, which
+// are contiguous) in ONE launch: a wave takes its tile's width (wave-uniform),
+// one LDS table and store buffer per wave serve every width, so the kernel's
+// registers and LDS are those of the widest.  The bulk of the FMA call then has
+// no side-stream lane kernels beside it, and no fork / join for them.
+__global__ __launch_bounds__(kBlock) void k_dequant_lanes_fma_any(
+    const dls_qtile *__restrict__ tiles, int ntiles, const uint8_t *__restrict__ Q, int64_t ldq,
+    const f32x2 *__restrict__ sz, SzLayout L, const int32_t *__restrict__ rows,
+    const float *__restrict__ w, int K, FastDiv d, float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) f32x2 ftab[kBlock / 64][kSpanMax + 1][64];
+    __shared__ __attribute__((aligned(16))) float xs[kBlock / 64][1024];
+    WaveTile wt;
+    if (!wave_tile(tiles, ntiles, wt)) return;
+    f32x2(*tab)[64] = ftab[threadIdx.x >> 6];
+    float *mine = xs[threadIdx.x >> 6];
+    const int slices = __builtin_amdgcn_readfirstlane((wt.t.len + 1023) >> 10);
+    auto run = [&](auto sgn_c, auto g_c) {
+        constexpr bool SG = decltype(sgn_c)::value;
+        constexpr int G = decltype(g_c)::value;
+        fma_lane_tile<SG, G, true>(wt, Q, ldq, sz, L, rows, w, K, d.b, out, tab, mine);
+    };
+    auto by_width = [&](auto sgn_c) {
+        if (slices >= 4)
+            run(sgn_c, std::integral_constant<int, 4>{});
+        else if (slices == 3)
+            run(sgn_c, std::integral_constant<int, 3>{});
+        else if (slices == 2)
+            run(sgn_c, std::integral_constant<int, 2>{});
+        else
+            run(sgn_c, std::integral_constant<int, 1>{});
+    };
+    if (wt.t.kind == 1)
+        by_width(std::true_type{});
+    else
+        by_width(std::false_type{});
 }
 
 // fp32 tensors (biases, norm weights) as their own group: tiles of <= 256
@@ -1580,6 +1631,25 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
         t += nfast[g];
         if (nfast[g] > 0 && (big < 0 || bytes(g) > bytes(big))) big = g;
     }
+    // FMA mode: the lane groups (4-7, contiguous in the table) as ONE launch of
+    // k_dequant_lanes_fma_any, on the caller's stream when their bytes are the most
+    const bool any = mode == DLS_FEDAVG_FMA && kQuantFmaAny;
+    int lanes_n = 0;
+    int64_t lanes_bytes = 0;
+    bool big_lanes = false;
+    if (any) {
+        for (int g = 4; g < 8; ++g) {
+            lanes_n += nfast[g];
+            lanes_bytes += bytes(g);
+        }
+        big = -1;
+        for (int g = 0; g < DLS_QTILE_GROUPS; ++g)
+            if ((g < 4 || g > 7) && nfast[g] > 0 && (big < 0 || bytes(g) > bytes(big))) big = g;
+        if (lanes_n > 0 && (big < 0 || lanes_bytes >= bytes(big))) {
+            big_lanes = true;
+            big = -1;
+        }
+    }
     const int ngen = ntiles - (int)nf;
     hipEvent_t fork = nullptr;
     hipEvent_t joins[DLS_QTILE_GROUPS + 1] = {};
@@ -1644,14 +1714,33 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
                                reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
         }
     };
-    for (int g = 0; g < DLS_QTILE_GROUPS; ++g)
+    auto launch_lanes_any = [&](hipStream_t s) {  // pieces of at most one generation
+        const void *kern = reinterpret_cast<const void *>(k_dequant_lanes_fma_any);
+        const int64_t slots = (int64_t)resident_blocks(kern, kBlock, 0) * wpb;
+        const int64_t np = (lanes_n + slots - 1) / slots;
+        const int64_t per = (lanes_n + np - 1) / np;
+        for (int64_t t0 = 0; t0 < lanes_n; t0 += per) {
+            const int m = (int)(lanes_n - t0 < per ? lanes_n - t0 : per);
+            hipLaunchKernelGGL(k_dequant_lanes_fma_any, dim3((unsigned)((m + wpb - 1) / wpb)),
+                               dim3(kBlock), 0, s, tg[4] + t0, m,
+                               reinterpret_cast<const uint8_t *>(Q), ldq,
+                               reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
+        }
+    };
+    for (int g = 0; g < DLS_QTILE_GROUPS; ++g) {
+        if (any && g >= 4 && g < 8) continue;
         if (g != big && nfast[g] > 0) launch_group(g, stream_for(false));
+    }
+    if (any && lanes_n > 0 && !big_lanes) launch_lanes_any(stream_for(false));
     if (ngen > 0)
         hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
                            dim3(kBlock), 0, stream_for(false), t, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
-    if (big >= 0) launch_group(big, st);
+    if (big_lanes)
+        launch_lanes_any(st);
+    else if (big >= 0)
+        launch_group(big, st);
     int rc = check_launch("dls_dequant_fedavg");
     for (int i = 0; i < nside; ++i) {
         hipError_t e = hipEventCreateWithFlags(&joins[i], hipEventDisableTiming);
