@@ -28,19 +28,17 @@ from .layout import ALIGN, ParameterLayout, _round_up
 
 TILE = 1024  # one wavefront slice: 64 lanes x 16 elements
 FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
-# multi-channel tiles (channel rows a multiple of 16): "adaptive" = the widest of
-# 4 / 2 / 1 KiB that spans at most 3 channel rows (4 KiB for rows >= 2048, 2 KiB
-# for rows >= 1024: every lane's channel constants stay in the kernel's staged
-# table), with rows shorter than ADAPTIVE_MIN_ROW left to the small-tile group (a
-# 1 KiB tile over more than the table's 4 channels is walked once per 4 channels
-# by the FMA lane kernel), or a fixed width in elements.  The store keeps one table per mode: the
+# multi-channel tiles (channel rows a multiple of 16): "adaptive" = per tensor the
+# tile width (4, 3, 2 or 1 KiB, or 1-4 whole channel rows, at most 4096 elements)
+# that needs the fewest tiles while every tile spans at most 4 channel rows (the
+# FMA lane kernel's staged table; a tile over more rows is walked once per 4), or
+# a fixed width in elements.  The store keeps one table per mode: the
 # exact kernel is bound by its instruction count at the clock the chip holds
 #  and runs fastest on 1 KiB tiles (4 waves per SIMD); the FMA mode
 # is bound by the stream and runs fastest on the adaptive ones (same-box A/B,
 # 1000 x ResNet-18: exact 2.01 vs 2.21 ms, FMA 1.96 vs 1.88 ms).
 LANE_TILE = 1024  # the exact mode's (and QuantLayout.tiles()' default)
 LANE_TILE_FMA = "adaptive"
-ADAPTIVE_MIN_ROW = 336  # elements: a 1 KiB lane tile then spans <= 4 channel rows
 F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
 SMALL_TILE = 256  # small int tiles: 64 lanes x 4 elements
 FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
@@ -62,6 +60,25 @@ def _int_repr(w):
 
 def is_quantized_entry(v):
     return isinstance(v, tuple) and len(v) == 3
+
+
+def _adaptive_lane_tile(rl, n):
+    """The FMA mode's lane-tile width for an n-element tensor of rl-element channel
+    rows (rl a multiple of 16): of 4096 / 3072 / 2048 / 1024 elements and 1-4 whole
+    rows (<= 4096), the one with the fewest tiles whose every tile spans <= 4 rows
+    (tiles start at multiples of the width from the tensor start); ties go to the
+    wider.  Whole rows always qualify, so every such tensor gets lane tiles: on
+    ResNet-18 the 3x3 convs take 4 KiB / 3,456 / 2,304-element tiles and the 1x1
+    shortcuts 1-4 rows, 2,986 waves in all (one generation of the FMA lane kernel
+    at 3 waves per SIMD)."""
+    def fits(t):
+        return all((e % rl + min(t, n - e) - 1) // rl + 1 <= 4 for e in range(0, n, t))
+    best = None
+    for t in sorted({4096, 3072, 2048, 1024} | {k * rl for k in (1, 2, 3, 4) if k * rl <= 4096},
+                    reverse=True):
+        if t % 16 == 0 and fits(t) and (best is None or -(-n // t) < -(-n // best)):
+            best = t
+    return best
 
 
 class QuantLayout:
@@ -125,9 +142,8 @@ class QuantLayout:
           tensors whose channel rows are a multiple of 16 elements (no lane's
           16-element chunk straddles two channels: 3x3 convs, fc layers) are cut
           into LANE_TILE-element tiles from their start, each lane in its own
-          channel (adaptive: 4 KiB tiles for rows >= 2048, 2 KiB for rows >= 1024,
-          1 KiB for rows >= ADAPTIVE_MIN_ROW: at most 4 channels per tile; shorter
-          rows go to the small tiles);
+          channel (adaptive: the width with the fewest tiles of <= 4 channel rows,
+          _adaptive_lane_tile);
         * fp32 tiles (group 8, <= F32_TILE elements): the fp32 tensors;
         * small int tiles (group 9, <= SMALL_TILE elements): the other int tensors
           with rows of at least 4 elements (a lane's 4 span <= 2 channels), except
@@ -149,9 +165,9 @@ class QuantLayout:
                                      j, cend))
                 continue
             lt = LANE_TILE if lane_tile is None else lane_tile
-            if kind and rl % 16 == 0 and (lt != "adaptive" or rl >= ADAPTIVE_MIN_ROW):
-                if lt == "adaptive":
-                    lt = 4096 if rl >= 2048 else (2048 if rl >= 1024 else TILE)
+            if lt == "adaptive" and kind and rl % 16 == 0:
+                lt = _adaptive_lane_tile(rl, n)  # None: not a lane-tile tensor
+            if kind and rl % 16 == 0 and lt is not None:
                 for e in range(0, n, lt):
                     lane_rows.append((off + e, src + e, min(lt, n - e), kind, cb + e // rl,
                                       rl, e % rl, cend))

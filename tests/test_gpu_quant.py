@@ -554,8 +554,8 @@ def test_dequant_fedavg_fma_lane_tiles_multipass(monkeypatch):
     tile, walked in passes of 4 channels while the other lanes read the table's
     zero row), int8 symmetric and uint8 with zero points, K across two 64-client
     chunks; every tensor within the north-star 1e-6 normwise of the exact
-    oracle.  The adaptive table never builds such tiles (rows < 336 go to the
-    small-tile group); a caller's fixed-width table may."""
+    oracle.  The adaptive table never builds such tiles (it picks widths of at
+    most 4 rows); a caller's fixed-width table may."""
     from distributed_learning_simulator_amd import _native, quant_store as qs
     from distributed_learning_simulator_amd.quant_store import QTILE_DTYPE, QuantizedClientStore
     monkeypatch.setattr(qs, "LANE_TILE_FMA", 1024)

@@ -71,8 +71,8 @@ def test_quant_layout_channel_aligned_tiles(lane_tile, monkeypatch):
     """Long channel rows (multiple of 64, last 1 KiB slice at least 7/8 full) get
     channel-aligned tiles of up to 4096 elements, grouped by slice count; other
     int tensors with rows a multiple of 16 get multi-channel (lane) tiles from their
-    start: LANE_TILE elements, or adaptive (4 KiB for rows >= 2048: conv and mid;
-    rows < ADAPTIVE_MIN_ROW, pw's 64, go to the small tiles)."""
+    start: LANE_TILE elements, or adaptive (the width with the fewest tiles of at
+    most 4 channel rows: 4 KiB for conv and mid, 4 rows = 256 elements for pw)."""
     from distributed_learning_simulator_amd import quant_store
     from distributed_learning_simulator_amd.quant_store import QuantLayout
     monkeypatch.setattr(quant_store, "LANE_TILE", lane_tile)
@@ -89,13 +89,13 @@ def test_quant_layout_channel_aligned_tiles(lane_tile, monkeypatch):
     if lane_tile == 1024:  # pw: one 512-element lane tile over 8 channel rows
         assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 0, 0, 0, 9 + 9 + 1) and nfast[8] == 0
         assert nfast[9] == (5 * 27 + 255) // 256  # c1 (rows of 27): small tiles
-    else:  # 9216-element tensors: 4096 + 4096 + 1024
-        assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 2 + 2, 0, 0, 1 + 1) and nfast[8] == 0
+    else:  # 9216-element tensors: 4096 + 4096 + 1024; pw: 2 x 4 rows of 64
+        assert nfast[:8] == (3 * 6, 0, 0, 3 + 2, 2 + 2, 0, 0, 1 + 1 + 2) and nfast[8] == 0
         lanes = t[sum(nfast[:4]):sum(nfast[:8])]
         # at most 4 channel rows per lane tile (the FMA kernel's staged table)
         assert max((int(r["row_pos"]) + int(r["len"]) - 1) // int(r["row_len"]) + 1
                    for r in lanes) <= 4
-        assert nfast[9] == (5 * 27 + 255) // 256 + 512 // 256  # c1 and pw: small tiles
+        assert nfast[9] == (5 * 27 + 255) // 256  # c1 (rows of 27): small tiles
     nf = sum(nfast)
     one = t[:sum(nfast[:4])]
     sl = [(int(r["len"]) + 1023) // 1024 for r in one]

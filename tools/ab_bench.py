@@ -204,6 +204,14 @@ def setup(dev, want=()):
         W["quant_r18_a"] = (qmode(tab_a, r1k, w1k, t1k, 0), nb, qo18)
         # DLS_FEDAVG_FMA (1e-6 tolerance mode) on the same 1000 clients
         W["quant_r18_fma"] = (qmode(tab_f, r1k, w1k, t1k, 1), nb, qo18)
+        # the previous adaptive rule (4 / 2 / 1 KiB by row length, rows < 336 to the
+        # small-int tiles): the tile-width policy A/B on the same kernels
+        keep_rule = qs._adaptive_lane_tile
+        qs._adaptive_lane_tile = lambda rl, n: (
+            4096 if rl >= 2048 else 2048 if rl >= 1024 else 1024 if rl >= 336 else None)
+        tab_old = table(qs.LANE_TILE_FMA)
+        qs._adaptive_lane_tile = keep_rule
+        W["quant_r18_fma_oldtab"] = (qmode(tab_old, r1k, w1k, t1k, 1), nb, qo18)
         # smaller fp32 / small-int tiles: more side-stream waves (latency-bound groups)
         for ft, stl in ((64, None), (64, 64), (128, 128)):
             tag = f"_f{ft}" + (f"s{stl}" if stl else "")
