@@ -125,8 +125,8 @@ def _stream(stream=None, like=None):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-CSRC_HASHED = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "shapley.hip", "infer.hip",
-               "dls_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
+CSRC_HASHED = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "quant_fma.hip", "shapley.hip",
+               "infer.hip", "dls_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
 
 
 def source_hash():
@@ -334,7 +334,8 @@ def bn_act_exact_nhwc(x, consts, residual=None, relu=True, out=None, inplace=Fal
 
 def bn_act_exact_nchw(x, consts, residual=None, relu=True, out=None, inplace=False, stream=None):
     """bn_act_exact_nhwc over an NCHW-contiguous [N, C, H, W] fp32 activation
-    (dls_bn_act_exact_nchw_f32; H*W a multiple of 4)."""
+    (dls_bn_act_exact_nchw_f32: float4 planes when H*W is a multiple of 4, one
+    element per lane otherwise)."""
     N, C, H, W = x.shape
     if not x.is_contiguous() or (residual is not None and not residual.is_contiguous()):
         raise RuntimeError("bn_act_exact_nchw: activations must be NCHW contiguous")

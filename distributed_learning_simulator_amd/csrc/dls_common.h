@@ -40,6 +40,16 @@ int device_cus();
 // Auxiliary stream number idx (0..63) on `parent`'s device for fork/join inside
 // one C-ABI call (nullptr on error).
 hipStream_t side_stream(hipStream_t parent, int idx);
+// Fork / join events of one C-ABI call on `parent` (idx 0: the fork, 1..: the
+// joins), created on first use and kept per (parent stream, idx), so a call
+// allocates nothing; nullptr on error.
+hipEvent_t call_event(hipStream_t parent, int idx);
+// FMA mode of dls_dequant_fedavg_mode: the int tiles of table groups 0-7 in
+// launch pieces of one wave per SIMD (quant_fma.hip).
+int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, const void *Q,
+                              int64_t ldq, const float *sz, int64_t sz_row, int64_t sz_chan,
+                              const int32_t *rows, const float *w, int32_t K, float N, float *out,
+                              hipStream_t st);
 
 inline hipStream_t as_stream(dls_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }

@@ -102,6 +102,29 @@ hipStream_t side_stream(hipStream_t parent, int idx) {
     return s;
 }
 
+hipEvent_t call_event(hipStream_t parent, int idx) {
+    // keyed by the parent stream: calls on one stream are ordered, so re-recording
+    // the same event for the next call is safe (a wait binds to the record that
+    // precedes it); calls on different streams use different events
+    static std::mutex mu;
+    static std::unordered_map<std::string, hipEvent_t> events;
+    char key[64];
+    snprintf(key, sizeof(key), "%p/%d", (void *)parent, idx);
+    std::lock_guard<std::mutex> g(mu);
+    auto it = events.find(key);
+    if (it != events.end()) return it->second;
+    int dev = 0, cur = 0;
+    if (hipStreamGetDevice(parent, &dev) != hipSuccess || hipGetDevice(&cur) != hipSuccess)
+        return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    hipEvent_t e = nullptr;
+    const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (rc != hipSuccess) return nullptr;
+    events[key] = e;
+    return e;
+}
+
 // One block of mantissas; `target` lets the compiler vectorise the fma / div
 // (the box's and this container's hosts are AVX-512 EPYC / Xeon parts).
 __attribute__((target("avx2,fma"))) static bool two_constant_block(uint32_t m0, uint32_t n, float b,

@@ -199,6 +199,25 @@ __global__ __launch_bounds__(kBnBlock) void k_bn_act_exact_nchw(const f32x4 *x, 
     }
 }
 
+// Planes whose size is not a multiple of 4 (e.g. a 7x7 layer3 plane of a 28x28
+// input: ResNet-18's adaptive pooling takes any input size): one element per
+// lane, the same arithmetic.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kBnBlock) void k_bn_act_exact_nchw1(const float *x, int64_t n, int C,
+                                                                 int64_t HW,
+                                                                 const float *__restrict__ consts,
+                                                                 const float *r, float *y) {
+    const int64_t stride = (int64_t)gridDim.x * kBnBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBnBlock + threadIdx.x; i < n; i += stride) {
+        const int c = (int)((i / HW) % C);
+        const float h = (x[i] - consts[c]) * consts[C + c];
+        float t = __builtin_fmaf(consts[2 * C + c], h, consts[3 * C + c]);
+        if (RES) t = t + r[i];
+        if (RELU) t = t > 0.f ? t : (t == t ? 0.f : t);
+        y[i] = t;
+    }
+}
+
 }  // namespace
 }  // namespace dls
 
@@ -208,11 +227,25 @@ extern "C" int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, i
                                          const float *consts, const float *residual, int32_t relu,
                                          float *y, dls_stream_t stream) {
     DLS_REQUIRE(x && consts && y, DLS_EINVAL, "dls_bn_act_exact_nchw_f32: null pointer");
-    DLS_REQUIRE(N > 0 && C > 0 && HW > 0 && HW % 4 == 0 && HW / 4 < (1 << 30), DLS_EINVAL,
-                "dls_bn_act_exact_nchw_f32: N=%lld C=%d HW=%lld (HW a multiple of 4)",
-                (long long)N, C, (long long)HW);
-    DLS_REQUIRE(aligned16(x) && aligned16(y) && (!residual || aligned16(residual)), DLS_ELAYOUT,
-                "dls_bn_act_exact_nchw_f32: 16-byte alignment");
+    DLS_REQUIRE(N > 0 && C > 0 && HW > 0 && HW / 4 < (1 << 30), DLS_EINVAL,
+                "dls_bn_act_exact_nchw_f32: N=%lld C=%d HW=%lld", (long long)N, C, (long long)HW);
+    if (HW % 4 != 0 || !aligned16(x) || !aligned16(y) || (residual && !aligned16(residual))) {
+        const int64_t n = N * C * HW;
+        int64_t blocks = (n + kBnBlock - 1) / kBnBlock;
+        if (blocks > 65536) blocks = 65536;
+        hipStream_t st1 = as_stream(stream);
+        const bool res1 = residual != nullptr;
+#define DLS_BN1(R_, A_)                                                                        \
+    hipLaunchKernelGGL((k_bn_act_exact_nchw1<R_, A_>), dim3((unsigned)blocks), dim3(kBnBlock), 0, \
+                       st1, x, n, (int)C, HW, consts, residual, y)
+        if (res1) {
+            if (relu) DLS_BN1(true, true); else DLS_BN1(true, false);
+        } else {
+            if (relu) DLS_BN1(false, true); else DLS_BN1(false, false);
+        }
+#undef DLS_BN1
+        return check_launch("dls_bn_act_exact_nchw_f32");
+    }
     const int64_t n4 = N * C * (HW / 4);
     const int HW4 = (int)(HW / 4);
     int64_t blocks = (n4 + (int64_t)kBnBlock * kBnUnroll - 1) / ((int64_t)kBnBlock * kBnUnroll);

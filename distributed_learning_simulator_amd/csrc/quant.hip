@@ -8,6 +8,7 @@
 // materialises the fp32 client tensors:
 //     out[e] (+)= fl(fl(fl(fl(q - zp[c]) * fl32(scale[c])) * fl32(n_i)) / fl32(N))
 // bit-exact in client order.  Algorithmic bytes: K*(Pq + 4*Pf + 8*C) + 4*P.
+#include <algorithm>
 #include <type_traits>
 
 #include "dls_common.h"
@@ -282,6 +283,19 @@ __device__ __forceinline__ float fma_coef(float s, float wk, float N) { return (
 #define DLS_QUANT_FMA_ANY 1
 #endif
 constexpr bool kQuantFmaAny = DLS_QUANT_FMA_ANY != 0;
+// FMA mode: groups 0-7 on the one-wave-per-SIMD kernel (quant_fma.hip); 0: the round-4
+// launches (k_dequant_fast_fma pieces + k_dequant_lanes_fma_any), an A/B knob
+#ifndef DLS_QUANT_FMA_STREAM
+#define DLS_QUANT_FMA_STREAM 1
+#endif
+constexpr bool kQuantFmaStream = DLS_QUANT_FMA_STREAM != 0;
+#ifndef DLS_QUANT_PIECE_WPS
+#define DLS_QUANT_PIECE_WPS 0  // > 0: the grouped kernels' launch pieces of this many waves per SIMD
+#endif
+constexpr int kQuantPieceWps = DLS_QUANT_PIECE_WPS;
+#ifndef DLS_QUANT_NTSTORE
+#define DLS_QUANT_NTSTORE 0  // 1: non-temporal output stores in store_tile (A/B knob)
+#endif
 
 #ifndef DLS_QUANT_PROBE
 #define DLS_QUANT_PROBE 0  // 1: stream-only timing probe (loads + a xor per dword; wrong output)
@@ -850,8 +864,13 @@ __device__ __forceinline__ void store_tile(const WaveTile &wt, float (&acc)[G][1
         for (int v = 0; v < 4; ++v) {
             const int e = 256 * v + 4 * __lane_id();
             const f32x4 x = *reinterpret_cast<const f32x4 *>(mine + e);
-            if (1024 * g + e < wt.lenpad)
-                *reinterpret_cast<f32x4 *>(out + wt.t.dst + 1024 * g + e) = x;
+            if (1024 * g + e < wt.lenpad) {
+                f32x4 *o = reinterpret_cast<f32x4 *>(out + wt.t.dst + 1024 * g + e);
+                if constexpr (DLS_QUANT_NTSTORE)
+                    __builtin_nontemporal_store(x, o);
+                else
+                    *o = x;
+            }
         }
     }
 }
@@ -1650,9 +1669,18 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
             big = -1;
         }
     }
+    // FMA mode: every int tile of groups 0-7 on quant_fma.hip's kernel on the
+    // caller's stream (quant_fma.hip); the fp32, small-int and general groups on
+    // side streams, launched first (few waves, each a long client walk)
+    const bool stream_fma = mode == DLS_FEDAVG_FMA && kQuantFmaStream;
+    if (stream_fma) {
+        big = -1;
+        big_lanes = false;
+    }
     const int ngen = ntiles - (int)nf;
+    // fork / join events cached per caller stream (dls_runtime.hip call_event):
+    // a call creates and destroys nothing
     hipEvent_t fork = nullptr;
-    hipEvent_t joins[DLS_QTILE_GROUPS + 1] = {};
     hipStream_t sides[DLS_QTILE_GROUPS + 1] = {};
     int nside = 0;
     bool forked = false;
@@ -1660,11 +1688,8 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
         if (empty) return st;
         if (!forked) {
             forked = true;
-            if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
-                hipEventRecord(fork, st) != hipSuccess) {
-                if (fork) (void)hipEventDestroy(fork);
-                fork = nullptr;
-            }
+            fork = call_event(st, 0);
+            if (fork && hipEventRecord(fork, st) != hipSuccess) fork = nullptr;
         }
         if (!fork) return st;
         hipStream_t s2 = side_stream(st, nside);
@@ -1703,8 +1728,9 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
             return;
         }
         const Kfn kern = kgroup[g][mode == DLS_FEDAVG_FMA ? 2 : (d.two ? 1 : 0)];
-        const int64_t slots = (int64_t)resident_blocks(reinterpret_cast<const void *>(kern), kBlock,
-                                                       0) * wpb;
+        int64_t slots = (int64_t)resident_blocks(reinterpret_cast<const void *>(kern), kBlock, 0) * wpb;
+        if (kQuantPieceWps > 0)  // pieces of this many waves per SIMD (A/B knob)
+            slots = std::min<int64_t>(slots, (int64_t)device_cus() * 4 * kQuantPieceWps);
         const int64_t np = (n + slots - 1) / slots;
         const int64_t per = (n + np - 1) / np;  // tiles per piece, <= slots
         for (int64_t t0 = 0; t0 < n; t0 += per) {
@@ -1728,33 +1754,35 @@ extern "C" int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles,
         }
     };
     for (int g = 0; g < DLS_QTILE_GROUPS; ++g) {
-        if (any && g >= 4 && g < 8) continue;
+        if ((any || stream_fma) && g >= 4 && g < 8) continue;
+        if (stream_fma && g < 4) continue;
         if (g != big && nfast[g] > 0) launch_group(g, stream_for(false));
     }
-    if (any && lanes_n > 0 && !big_lanes) launch_lanes_any(stream_for(false));
+    if (any && !stream_fma && lanes_n > 0 && !big_lanes) launch_lanes_any(stream_for(false));
     if (ngen > 0)
         hipLaunchKernelGGL(k_dequant_general, dim3((unsigned)((ngen + wpb - 1) / wpb)),
                            dim3(kBlock), 0, stream_for(false), t, ngen,
                            reinterpret_cast<const uint8_t *>(Q), ldq, F, ldf,
                            reinterpret_cast<const f32x2 *>(sz), L, rows, weight, (int)K, d, out);
-    if (big_lanes)
+    int rc = DLS_OK;
+    if (stream_fma)
+        rc = launch_dequant_fma_stream(tiles, nfast, Q, ldq, sz, sz_row, sz_chan, rows, weight, K,
+                                       total, out, st);
+    else if (big_lanes)
         launch_lanes_any(st);
     else if (big >= 0)
         launch_group(big, st);
-    int rc = check_launch("dls_dequant_fedavg");
+    if (rc == DLS_OK) rc = check_launch("dls_dequant_fedavg");
     for (int i = 0; i < nside; ++i) {
-        hipError_t e = hipEventCreateWithFlags(&joins[i], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventRecord(joins[i], sides[i]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, joins[i], 0);
+        hipEvent_t join = call_event(st, 1 + i);
+        hipError_t e = join ? hipEventRecord(join, sides[i]) : hipErrorOutOfMemory;
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, join, 0);
         if (e != hipSuccess) {  // the caller's stream must not run ahead of the side work
             (void)hipStreamSynchronize(sides[i]);
             set_error("dls_dequant_fedavg: stream join failed: %s", hipGetErrorString(e));
             rc = (int)e;
         }
     }
-    for (int i = 0; i < nside; ++i)
-        if (joins[i]) (void)hipEventDestroy(joins[i]);
-    if (fork) (void)hipEventDestroy(fork);  // released once the enqueued record / wait complete
     return rc;
 }
 

@@ -496,9 +496,16 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
     if (CB <= 12) {
         if (kVoteWPC > 0) {
             // exactly kVoteWPC waves per CU, near-equal ranges of up to 64 G groups
-            const int64_t waves = (int64_t)kVoteWPC * device_cus();
-            const int64_t r = (vote_groups + waves - 1) / waves;
-            if (r > 64 && r <= 64 * kVoteG) {
+            int64_t waves = (int64_t)kVoteWPC * device_cus();
+            int64_t r = (vote_groups + waves - 1) / waves;
+            if (r > 64 * kVoteG) {
+                // models past 64 kVoteG groups per wave (P > ~16.7M on 256 CUs, e.g.
+                // VGG-16): a multiple of kVoteWPC waves per CU, so that every wave
+                // keeps the wide layout (G = kVoteG at most) instead of G = 1
+                waves *= (r + 64 * kVoteG - 1) / (64 * kVoteG);
+                r = (vote_groups + waves - 1) / waves;
+            }
+            if (r > 64) {
                 nwaves = waves;
                 G = (int)((r + 63) / 64);
                 wpb = kVoteWPB;

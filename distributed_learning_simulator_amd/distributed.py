@@ -124,13 +124,15 @@ class ShardedFedServer(_ShardedMixin, FedServer):
     ``exchange="allreduce"`` (default): each rank reduces its own clients with the
     global N, then a chunked fp32 SUM all-reduce — one P-element exchange,
     normwise ~1e-7 of the exact mean.  ``exchange="alltoall"``: bit-exact for any
-    number of ranks: every rank owns a parameter slice, every
-    client's slice moves from its rank's store row straight to its owner
-    (point-to-point sends batched into one RCCL group, no staging copy), each
-    rank runs the reference-order kernel over ALL K clients on its slice, and an
+    number of ranks: every rank owns a parameter slice; the store
+    is slice-major, so ONE ``all_to_all_single`` sends slice d of every row of the
+    rank's store to rank d straight from the store (no staging copy); each rank
+    runs the reference-order kernel over ALL K clients on its slice, and an
     all-gather assembles the mean — bits identical to one FedServer that saw the
-    clients in the same order, at the cost of moving (world-1)/world of the
-    client rows instead of one P-vector.
+    clients in the same order.  Its traffic is the whole store: every call moves
+    capacity x P fp32 per rank (its released and unused rows and its own slice
+    included), whatever the subset size — against one P-vector for the
+    all-reduce.
 
     ``order`` (alltoall only) is the client order of the sum: ``"arrival"`` (the
     reference's: ``self.parameters.keys()`` in insertion order,
@@ -248,12 +250,6 @@ class ShardedFedServer(_ShardedMixin, FedServer):
             dist.all_gather_into_tensor(out, part, group=self.group)
         return out[:P]
 
-    def _peer(self, rank):
-        """Global rank of ``rank`` in self.group (P2P ops take global ranks)."""
-        if self.group is None:
-            return rank
-        return dist.get_global_rank(self.group, rank)
-
     def get_subset_model(self, client_subset):
         if not client_subset:
             return self.prev_model
@@ -280,6 +276,12 @@ class ShardedFedServer(_ShardedMixin, FedServer):
 
 
 class ShardedFedQuantServer(_ShardedMixin, FedQuantServer):
+    """FedQuantServer over all ranks: each rank dequantizes and averages its own
+    clients with the global N, column chunk by column chunk (the store's tile
+    sub-tables, ``QuantizedClientStore.fedavg(cols=...)``), and chunk c's SUM
+    all-reduce is on the wire while chunk c+1 is reduced — the same pipeline as
+    ShardedFedServer's, in the server's ``aggregation_mode``."""
+
     def __init__(self, group=None, chunks=3, **kwargs):
         self._init_shard(kwargs["worker_number"], group, chunks)
         super().__init__(**kwargs)
@@ -292,9 +294,17 @@ class ShardedFedQuantServer(_ShardedMixin, FedQuantServer):
         total = global_sample_count(ns, self.device, self.group)
         store = self.parameters.store
         out = torch.zeros(store.layout.P, dtype=torch.float32, device=self.device)
+        produce = None
         if ids:
-            store.fedavg([self.parameters.row_of(i) for i in ids], ns, out=out, total=total)
-        allreduce_chunked(out, self.chunks, self.group)
+            from .aggregation import _f32, _i32
+            from .servers.fed_server import _MODES
+            r = _i32([self.parameters.row_of(i) for i in ids], self.device)
+            w = _f32(ns, self.device)
+            mode = _MODES[self.aggregation_mode]
+
+            def produce(c0, c1):  # reduce chunk c while chunk c-1 is on the wire
+                store.fedavg(r, w, out=out, total=total, mode=mode, cols=(c0, c1))
+        allreduce_chunked(out, self.chunks, self.group, produce=produce)
         return store.layout.views(out)
 
 

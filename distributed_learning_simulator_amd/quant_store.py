@@ -39,6 +39,8 @@ FAST_TILE = 4096  # one-channel tiles: up to 4 slices per wavefront
 # 1000 x ResNet-18: exact 2.01 vs 2.21 ms, FMA 1.96 vs 1.88 ms).
 LANE_TILE = 1024  # the exact mode's (and QuantLayout.tiles()' default)
 LANE_TILE_FMA = "adaptive"
+LANE_TILE_MAX = 4096  # the adaptive widths' bound (elements)
+FMA_ONE_CHANNEL = False  # the FMA table's long-row tensors: one-channel tiles (True) or lane tiles
 F32_TILE = 256  # fp32 tensors: 64 lanes x 4 elements
 SMALL_TILE = 256  # small int tiles: 64 lanes x 4 elements
 FAST_WASTE = 16  # one-channel tiles need their rows' idle lanes <= row / FAST_WASTE (0: none)
@@ -74,8 +76,9 @@ def _adaptive_lane_tile(rl, n):
     def fits(t):
         return all((e % rl + min(t, n - e) - 1) // rl + 1 <= 4 for e in range(0, n, t))
     best = None
-    for t in sorted({4096, 3072, 2048, 1024} | {k * rl for k in (1, 2, 3, 4) if k * rl <= 4096},
-                    reverse=True):
+    cap = LANE_TILE_MAX
+    for t in sorted({x for x in (8192, 6144, 4096, 3072, 2048, 1024) if x <= cap} |
+                    {k * rl for k in (1, 2, 3, 4) if k * rl <= cap}, reverse=True):
         if t % 16 == 0 and fits(t) and (best is None or -(-n // t) < -(-n // best)):
             best = t
     return best
@@ -129,7 +132,7 @@ class QuantLayout:
                 return False
         return True
 
-    def tiles(self, lane_tile=None):
+    def tiles(self, lane_tile=None, one_channel=True):
         """(table, nfast): wave tiles; nfast = counts of the 10 grouped kinds at the
         head of the table (dls_hip.h DLS_QTILE_GROUPS), then the general tiles.
         ``lane_tile``: the multi-channel tiles' width (default LANE_TILE).
@@ -148,7 +151,13 @@ class QuantLayout:
         * small int tiles (group 9, <= SMALL_TILE elements): the other int tensors
           with rows of at least 4 elements (a lane's 4 span <= 2 channels), except
           their 1 KiB pieces that lie inside one channel (one-channel group 3);
-        * general tiles (<= TILE elements): int tensors with rows shorter than 4."""
+        * general tiles (<= TILE elements): int tensors with rows shorter than 4.
+
+        ``one_channel=False`` (the FMA mode's table, FMA_ONE_CHANNEL): long-row
+        tensors are lane-tiled too — contiguous tiles across the row boundaries
+        (a 4096-element tile over a 25,088-element fc row spans <= 2 channels), so
+        no row leaves a part-filled tail tile (VGG-16's fc1: 4,096 half-empty
+        512-element tiles otherwise)."""
         rows, lane_rows, f32_rows, small_rows = [], [], [], []
         for i, kind in enumerate(self.kinds):
             n = self.layout.numels[i]
@@ -156,7 +165,7 @@ class QuantLayout:
             off, src, cb = self.layout.offsets[i], self.src[i], self.chan_base[i]
             cend = cb + self.channels[i] if kind else 0
             waste = -rl % TILE  # idle lanes of the row's last slice
-            if kind and rl >= TILE and rl % 64 == 0 and (
+            if one_channel and kind and rl >= TILE and rl % 64 == 0 and (
                     waste == 0 if FAST_WASTE == 0 else FAST_WASTE * waste <= rl):
                 for c in range(self.channels[i]):
                     for j in range(0, rl, FAST_TILE):
@@ -199,7 +208,8 @@ class QuantLayout:
             return (r[2] + 63) // 64 * 64 // TILE + ((r[2] + 63) // 64 * 64 % TILE != 0)
 
         fast = [[r for r in rows if one_channel(r) and slices(r) == g] for g in (4, 3, 2, 1)]
-        fast += [[r for r in lane_rows if slices(r) == g] for g in (4, 3, 2, 1)]
+        # group 4: lane tiles of 4 KiB slices or more (FMA tables: up to LANE_TILE_MAX)
+        fast += [[r for r in lane_rows if min(slices(r), 4) == g] for g in (4, 3, 2, 1)]
         fast += [f32_rows, small_rows]
         rest = [r for r in rows if not one_channel(r)]
         assert all(r[2] <= TILE for r in rest)
@@ -220,9 +230,12 @@ class QuantizedClientStore:
         t, self.nfast = ql.tiles()
         self.ntiles = len(t)
         self.tiles = torch.from_numpy(t.view(np.uint8).copy()).to(self.device)
-        tf, self.nfast_fma = ql.tiles(LANE_TILE_FMA)
+        tf, self.nfast_fma = ql.tiles(LANE_TILE_FMA, one_channel=FMA_ONE_CHANNEL)
         self.ntiles_fma = len(tf)
         self.tiles_fma = torch.from_numpy(tf.view(np.uint8).copy()).to(self.device)
+        self._host_tables = {_native.FEDAVG_EXACT: (t, self.nfast),
+                             _native.FEDAVG_FMA: (tf, self.nfast_fma)}
+        self._col_tables = {}
         self._free = list(range(cap))[::-1]
 
     @property
@@ -269,25 +282,58 @@ class QuantizedClientStore:
                 self.F[row, ql.src[i]:ql.src[i] + n].copy_(v.reshape(-1).float(),
                                                            non_blocking=True)
 
-    def fedavg(self, rows, ns, out=None, total=None, mode=_native.FEDAVG_EXACT):
+    def fedavg(self, rows, ns, out=None, total=None, mode=_native.FEDAVG_EXACT, cols=None):
         """Dequant + weighted mean of the rows (dls_dequant_fedavg_mode): EXACT is
-        bit-exact with the reference's dequant-then-average, FMA within 1e-6."""
+        bit-exact with the reference's dequant-then-average, FMA within 1e-6.
+
+        ``rows`` / ``ns``: sequences, or device int32 / fp32 tensors (a caller that
+        makes several calls over the same clients converts them once).  ``cols =
+        (c0, c1)``: only the tiles whose first output element lies in [c0, c1)
+        (``out`` is still the whole P-element row; a tile starting in the range may
+        end past c1, so the range's elements are final once every range before it
+        has run too) — the sharded server reduces the column chunks in order while
+        the previous chunk's all-reduce is on the wire."""
         if out is None:
             out = torch.empty(self.layout.P, dtype=torch.float32, device=self.device)
-        if total is None:
-            total = sum(int(n) for n in ns)
-        rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
-        w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
-        tiles, ntiles, nfast = self.table(mode)
+        if torch.is_tensor(rows):
+            rows_t = rows
+        else:
+            rows_t = torch.tensor(list(rows), dtype=torch.int32).to(self.device)
+        if torch.is_tensor(ns):
+            w_t = ns
+            if total is None:
+                total = float(ns.sum())
+        else:
+            w_t = torch.tensor([int(n) for n in ns], dtype=torch.float32).to(self.device)
+            if total is None:
+                total = sum(int(n) for n in ns)
+        tiles, ntiles, nfast = self.table(mode, cols)
+        if ntiles == 0:
+            return out
         _native.dequant_fedavg(tiles, ntiles, nfast, self.Q, self.F, self.sz, rows_t, w_t,
                                float(total), out, mode=mode)
         return out
 
-    def table(self, mode=_native.FEDAVG_EXACT):
-        """(tiles, ntiles, nfast) the fused kernel takes in this mode."""
-        if mode == _native.FEDAVG_FMA:
-            return self.tiles_fma, self.ntiles_fma, self.nfast_fma
-        return self.tiles, self.ntiles, self.nfast
+    def table(self, mode=_native.FEDAVG_EXACT, cols=None):
+        """(tiles, ntiles, nfast) the fused kernel takes in this mode; ``cols``: the
+        sub-table of the tiles starting in [c0, c1), groups kept in table order
+        (built on the host once per (mode, range) and cached)."""
+        if cols is None:
+            if mode == _native.FEDAVG_FMA:
+                return self.tiles_fma, self.ntiles_fma, self.nfast_fma
+            return self.tiles, self.ntiles, self.nfast
+        key = (int(mode), int(cols[0]), int(cols[1]))
+        hit = self._col_tables.get(key)
+        if hit is None:
+            t, nfast = self._host_tables[int(mode)]
+            ends = np.cumsum(list(nfast))
+            group = np.searchsorted(ends, np.arange(len(t)), side="right")  # len(nfast): general
+            keep = (t["dst"] >= cols[0]) & (t["dst"] < cols[1])
+            sub = t[keep]
+            nsub = tuple(int(np.count_nonzero(keep & (group == g))) for g in range(len(nfast)))
+            dev = torch.from_numpy(sub.view(np.uint8).copy()).to(self.device)
+            hit = self._col_tables[key] = (dev, len(sub), nsub)
+        return hit
 
     def dequantize(self, row):
         """One client's fp32 dict (the reference's _process_client_parameter output)."""

@@ -136,12 +136,15 @@ class Inferencer:
         if bn is None:
             return True
         g = torch.Generator().manual_seed(0)
-        x = (torch.randn(2, bn.num_features, 6, 6, generator=g) * 3).to(self.device)
-        x = x.contiguous(memory_format=self._memory_format())
         consts = torch.empty(4 * bn.num_features, device=self.device)
         _native.bn_fold_exact(bn, consts)
-        y = _native.bn_act_exact(x, consts, relu=False)
-        return torch.equal(y.view(torch.int32), bn(x).view(torch.int32))
+        for hw in (6, 7):  # float4 planes, and planes of an odd size (the per-element path)
+            x = (torch.randn(2, bn.num_features, hw, hw, generator=g) * 3).to(self.device)
+            x = x.contiguous(memory_format=self._memory_format())
+            y = _native.bn_act_exact(x, consts, relu=False)
+            if not torch.equal(y.view(torch.int32), bn(x).view(torch.int32)):
+                return False
+        return True
 
     def _fused_forward(self, X):
         if not (self.fused_eval and X.dim() == 4 and torch.device(self.device).type == "cuda"):

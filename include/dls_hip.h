@@ -206,11 +206,13 @@ int dls_dequant_fedavg(const dls_qtile *tiles, int32_t ntiles, const int32_t *nf
 /* The same with a mode (DLS_FEDAVG_EXACT: dls_dequant_fedavg, bit-exact;
  * DLS_FEDAVG_FMA: the int tiles of groups 0-7 accumulate out = fma(q - zp, c,
  * out) with one constant per (client, channel) c = fl(fl(scale * n_i) / N)
- * (q - zp exact; the subtraction skipped for chunks of zero points 0, the QAT
- * worker's symmetric qint8) — one packed op per element pair instead of five,
- * a different rounding of each term: within the north-star's 1e-6 FedAvg
- * tolerance (normwise), not bit-exact; groups 8-9 and the general tiles run
- * their exact kernels). */
+ * (q - zp exact) — a conversion and two packed ops per element pair instead of
+ * the exact mode's six, a different rounding of each term: within the
+ * north-star's 1e-6 FedAvg tolerance (normwise), not bit-exact; groups 8-9 and
+ * the general tiles run their exact kernels.  Groups 0-7 run on one kernel in
+ * launch pieces of one wave per SIMD, so the one-channel / lane split does not
+ * matter here: the store's FMA table lane-tiles every int tensor whose channel
+ * rows are a multiple of 16 elements, long rows included). */
 int dls_dequant_fedavg_mode(const dls_qtile *tiles, int32_t ntiles, const int32_t *nfast,
                             const void *Q, int64_t ldq, const float *F, int64_t ldf,
                             const float *sz, int64_t sz_row, int64_t sz_chan, const int32_t *rows,
@@ -268,8 +270,11 @@ int dls_bn_fold_exact_f32(const float *weight, const float *bias, const float *m
 int dls_bn_act_exact_nhwc_f32(const float *x, int64_t rows, int32_t C, const float *consts,
                               const float *residual, int32_t relu, float *y, dls_stream_t stream);
 /* The same exact pass over an NCHW (contiguous) [N, C, H, W] fp32 tensor, HW =
- * H*W a multiple of 4 (MIOpen's deterministic convolutions are NCHW ones: the
- * reproducible utility evaluation runs in that layout).  y may alias x. */
+ * H*W (MIOpen's deterministic convolutions are NCHW ones: the reproducible
+ * utility evaluation runs in that layout): float4 planes when HW is a multiple
+ * of 4 and the pointers 16-byte aligned, one element per lane otherwise (any
+ * input size: ResNet-18's adaptive pooling takes 28x28, whose layer3 planes are
+ * 7x7).  y may alias x. */
 int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
                               const float *consts, const float *residual, int32_t relu, float *y,
                               dls_stream_t stream);

@@ -160,6 +160,53 @@ def _shapley_worker(rank, world, port, outq):
     dist.destroy_process_group()
 
 
+def _quant_payloads(K):
+    """Synthetic fed_quant client payloads (ref servers/fed_quant_server.py:26-32):
+    per-channel int8 / uint8 tensors with their (scale, zero point) and fp32 ones,
+    sized so that the store's column chunks split tensors and tiles."""
+    rng = np.random.RandomState(11)
+    shapes = [("conv.weight", (16, 8, 3, 3), 1), ("conv.bias", (16,), 0),
+              ("fc.weight", (24, 600), 1), ("fc.bias", (24,), 0), ("u8.weight", (20, 50), 2)]
+    out = []
+    for _ in range(K):
+        d = {}
+        for name, shape, kind in shapes:
+            if kind == 0:
+                d[name] = torch.from_numpy(rng.standard_normal(shape).astype(np.float32))
+                continue
+            lo, hi = (-128, 128) if kind == 1 else (0, 256)
+            q = rng.randint(lo, hi, size=shape).astype(np.int8 if kind == 1 else np.uint8)
+            sc = rng.uniform(1e-3, 1e-2, size=shape[0])
+            zp = np.zeros(shape[0], np.int64) if kind == 1 else rng.randint(100, 150, shape[0])
+            d[name] = (torch.from_numpy(q), torch.from_numpy(sc), torch.from_numpy(zp))
+        out.append(d)
+    return shapes, out
+
+
+def _fed_quant_worker(rank, world, port, outq):
+    _init(rank, world, port)
+    from distributed_learning_simulator_amd.distributed import ShardedFedQuantServer
+    K = 6
+    shapes, payloads = _quant_payloads(K)
+    res = {}
+    for chunks in (3, 1):
+        server = ShardedFedQuantServer(tester=None, worker_number=K, synchronous=True,
+                                       device=torch.device("cpu"), chunks=chunks)
+        q = server.worker_data_queue
+        for w in server.local_worker_ids:
+            q.get_result(consumer=w, timeout=30)
+        for wid in server.local_worker_ids:
+            q.add_task((wid, 10 + 3 * wid, payloads[wid]))
+        for w in server.local_worker_ids:
+            q.get_result(consumer=w, timeout=30)
+        agg = server.last_aggregate
+        res[chunks] = np.concatenate([agg[nm].reshape(-1).numpy() for nm, _, _ in shapes])
+        if chunks == 3:  # the pipelined path really ran in 3 column ranges
+            assert len(server.parameters.store._col_tables) == 3
+    outq.put((rank, res[3], res[1]))
+    dist.destroy_process_group()
+
+
 def _spawn(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -289,3 +336,27 @@ def test_sharded_gtg_clients_sharded(world):
     for _, sv, _n in out:
         for k, v in case["sv"].items():
             assert abs(sv[int(k)] - v) <= 1e-12
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fed_quant_chunked_pipeline(world):
+    """ShardedFedQuantServer reduces its clients column chunk by column chunk (tile
+    sub-tables) while the previous chunk's all-reduce is on the wire: the bits
+    equal the unchunked sharded result, every rank agrees, and the aggregate is the
+    dequant-then-FedAvg of all clients within the north-star 1e-6."""
+    out = _spawn(_fed_quant_worker, world)
+    for _, chunked, whole in out:
+        assert np.array_equal(chunked.view(np.uint32), out[0][1].view(np.uint32))  # ranks agree
+        if world == 2:  # a + b == b + a: the per-tile partials and their sum are the same bits
+            assert np.array_equal(chunked.view(np.uint32), whole.view(np.uint32))
+        else:  # 3 partials: the collective's summation order depends on the message size
+            assert np.linalg.norm(chunked - whole) <= 1e-7 * np.linalg.norm(whole)
+    from oracle.quant import dequant_fedavg
+    K = 6
+    shapes, payloads = _quant_payloads(K)
+    clients = [{nm: (tuple(x.numpy() for x in v) if isinstance(v, tuple) else v.numpy())
+                for nm, v in p.items()} for p in payloads]
+    ref = dequant_fedavg(clients, [10 + 3 * w for w in range(K)], list(range(K)),
+                         [(nm, shape) for nm, shape, _ in shapes])
+    got = out[0][1]
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-6

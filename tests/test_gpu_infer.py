@@ -233,3 +233,32 @@ def test_utility_is_a_function_of_the_model():
     # the module's own forward under the same flags: the same bits
     plain = Inferencer(model, (X, y), device=dev, fused_eval=False)
     assert torch.equal(plain.logits().view(torch.int32), la.view(torch.int32))
+
+
+def test_inferencer_odd_plane_sizes():
+    """ResNet-18's adaptive pooling takes any input size; a 28x28 input
+    reaches layer3 as 7x7 planes (49 elements, not a multiple of 4), which the
+    NCHW exact pass runs element-wise: the default Inferencer's logits equal the
+    module's own forward, bit for bit."""
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    torch.manual_seed(3)
+    model = ResNet18().to(dev)
+    X, y = synthetic_classification(512, (3, 28, 28), seed=5)
+    a = Inferencer(model, (X, y), device=dev)
+    la = a.logits()
+    assert a._fused_checked == (torch.contiguous_format, True)
+    plain = Inferencer(model, (X, y), device=dev, fused_eval=False)
+    assert torch.equal(plain.logits().view(torch.int32), la.view(torch.int32))
+    # the kernel alone on odd planes, with a residual and ReLU, vs torch
+    g = torch.Generator().manual_seed(1)
+    bn = _bn(24, g)
+    consts = torch.empty(4 * 24, device=dev)
+    _native.bn_fold_exact(bn, consts)
+    x = torch.randn(3, 24, 7, 5, generator=g).to(dev)
+    r = torch.randn(3, 24, 7, 5, generator=g).to(dev)
+    got = _native.bn_act_exact(x, consts, residual=r, relu=True)
+    with torch.no_grad():
+        ref = torch.relu(bn(x) + r)
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))

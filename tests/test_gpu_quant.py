@@ -548,6 +548,61 @@ def test_dequant_fedavg_lane_tiles_resnet_shapes(K):
                 assert err <= 1e-6, (name, err)
 
 
+@pytest.mark.parametrize("lane_tile", ["adaptive", 4096])
+def test_dequant_fedavg_exact_wide_lane_tiles(monkeypatch, lane_tile):
+    """the EXACT mode on lane tiles of 2-4 KiB (k_dequant_lanes<4|3|2>,
+    reachable through the ABI with any caller table): the adaptive widths and a
+    fixed 4096-element table, with a client whose scale leaves the fast-division
+    range (the per-client fallback) and a tile over more than 4 channels (rows of
+    16: the per-client gather path); bit-exact vs the oracle, K across two
+    64-client chunks."""
+    from distributed_learning_simulator_amd import _native, quant_store as qs
+    from distributed_learning_simulator_amd.quant_store import QTILE_DTYPE, QuantizedClientStore
+    monkeypatch.setattr(qs, "LANE_TILE", lane_tile)
+    K = 70
+    g = torch.Generator().manual_seed(41)
+    shapes = {"l1": (8, 64, 3, 3), "l2": (16, 128, 3, 3), "l3": (6, 256, 3, 3),
+              "pw16": (64, 16, 1, 1), "fc": (10, 512)}
+    payloads, n = [], []
+    for k in range(K):
+        p = {}
+        for name, s_ in shapes.items():
+            C = s_[0]
+            if name == "l2":  # uint8 with zero points
+                p[name] = (torch.randint(0, 256, s_, generator=g, dtype=torch.uint8),
+                           torch.rand(C, generator=g, dtype=torch.float64) * 1e-3 + 1e-5,
+                           torch.randint(0, 256, (C,), generator=g))
+            else:
+                sc = torch.rand(C, generator=g, dtype=torch.float64) * 1e-2 + 1e-4
+                if k == K // 2 and name in ("l1", "pw16"):
+                    sc[2] = 3e30  # this client takes the fallback
+                p[name] = (torch.randint(-128, 128, s_, generator=g, dtype=torch.int8), sc,
+                           torch.zeros(C, dtype=torch.int64))
+        payloads.append(p)
+        n.append(int(torch.randint(1, 1000, (1,), generator=g)))
+    store = QuantizedClientStore(payloads[0], dev, capacity=K)
+    t = store.tiles.cpu().numpy().view(QTILE_DTYPE)
+    assert sum(store.nfast[4:7]) > 0  # 2-4 KiB lane tiles in the EXACT table
+    lanes = t[sum(store.nfast[:4]):sum(store.nfast[:8])]
+    span = (lanes["row_pos"] + lanes["len"] - 1) // lanes["row_len"] + 1
+    if lane_tile == 4096:
+        assert span.max() > 4  # the per-client gather path
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    order = list(torch.randperm(K, generator=g).tolist())
+    layout = [(k, tuple(v[0].shape)) for k, v in payloads[0].items()]
+    clients = [{k: tuple(t_.numpy() for t_ in v) for k, v in p.items()} for p in payloads]
+    ref = oquant.dequant_fedavg(clients, n, order, layout)
+    full = torch.full((store.layout.P,), float("nan"), device=dev)
+    out = store.layout.views(store.fedavg([rows[i] for i in order], [n[i] for i in order],
+                                          out=full, mode=_native.FEDAVG_EXACT))
+    assert_padding_zero(store.layout, full)
+    assert same_bits(flat(out, layout), ref)
+
+
 def test_dequant_fedavg_fma_lane_tiles_multipass(monkeypatch):
     """FMA-mode lane tiles over more channels than the kernel's staged table (4):
     1 KiB lane tiles on rows of 16, 48 and 64 elements (up to 64 channels per

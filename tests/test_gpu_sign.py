@@ -298,3 +298,33 @@ def test_vote_balanced_wave_ranges(P):
     rows = torch.tensor([12, 0, 5, 7, 3], dtype=torch.int32, device=dev)
     _native.sign_vote_count(planes, rows, len(rows), P, c)
     assert torch.equal(c, S[rows.long()].sum(0).int())
+
+
+def test_vote_wide_layout_very_large_model():
+    """past 64 x 4 vote groups per wave (P > ~16.7M parameters on 256
+    CUs; here P = 70M, VGG-16-scale) the vote keeps the wide per-wave layout with
+    a multiple of the waves per CU; the signs and packed vote equal torch's vote
+    computed from the same planes (bit unpacking on the GPU), on every parameter."""
+    from distributed_learning_simulator_amd import _native
+    K, P = 24, 70_000_000
+    W = _native.sign_words(P)
+    g = torch.Generator(device=dev).manual_seed(77)
+    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    planes[:, 1::2] &= ~planes[:, 0::2]  # no NaN codes
+    planes[:, 2 * ((P + 63) // 64):] = 0
+    sign = torch.empty(P, device=dev)
+    vote = torch.full((W,), 0x55, dtype=torch.int64, device=dev)
+    _native.sign_vote(planes, None, K, P, sign, vote_planes=vote)
+    pos, neg = planes[:, 0::2], planes[:, 1::2]  # [K, groups of 64]
+    ng = (P + 63) // 64
+    counts = torch.empty((ng, 64), dtype=torch.int32, device=dev)
+    for j in range(64):
+        bp = ((pos[:, :ng] >> j) & 1).sum(0, dtype=torch.int32)
+        bn = ((neg[:, :ng] >> j) & 1).sum(0, dtype=torch.int32)
+        counts[:, j] = bp - bn
+    ref = torch.sign(counts.reshape(-1)[:P].float())
+    assert torch.equal(sign.view(torch.int32), ref.view(torch.int32))
+    v2 = torch.zeros(W, dtype=torch.int64, device=dev)
+    s2 = torch.empty(P, device=dev)
+    _native.sign_from_counts(counts.reshape(-1)[:P].contiguous(), P, s2, v2)
+    assert torch.equal(vote, v2)

@@ -92,7 +92,7 @@ def setup(dev, want=()):
         W["pack"] = (lambda L: L.dls_sign_pack_f32(ptr(X), P, 16, P, ptr(pk), Wd, None, stream()),
                      16 * (P * 4 + Wd * 8))
     if {"quant", "quant_fma", "quant1k", "quant_samerow", "quant_w0", "quant_w8",
-            "quant_w16"} & set(want):
+            "quant_w16"} & set(want) or any(x.startswith("quant_fma") for x in want):
         from distributed_learning_simulator_amd.quant_store import QuantizedClientStore
         template = {}
         for name, s in vgg16():
@@ -134,6 +134,82 @@ def setup(dev, want=()):
             ptr(tf), ntf, nfast_arg(L, nff), ptr(st.Q), st.Q.stride(0), ptr(st.F), st.F.stride(0),
             ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2, ptr(rows), ptr(w), 100, tot, 1,
             ptr(qo), stream()), 100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel)
+        # FMA tables with narrower tiles: one-channel FAST_TILE and the adaptive
+        # lane widths capped at 2 / 1 KiB (for kernel builds with DLS_FMA_GMAX < 4)
+        from distributed_learning_simulator_amd import quant_store as qsv
+
+        def capped_table(qlay, cap):
+            keep = (qsv.FAST_TILE, qsv.LANE_TILE_MAX)
+            qsv.FAST_TILE, qsv.LANE_TILE_MAX = cap, cap
+            tt, nft = qlay.tiles(qsv.LANE_TILE_FMA)
+            qsv.FAST_TILE, qsv.LANE_TILE_MAX = keep
+            return torch.from_numpy(tt.view(np.uint8).copy()).to(dev), len(tt), nft
+        for cap in (3072, 2048, 1024):
+            tc, ntc, nfc = capped_table(ql, cap)
+            W[f"quant_fma_t{cap // 1024}"] = (
+                lambda L, tc=tc, ntc=ntc, nfc=nfc: L.dls_dequant_fedavg_mode(
+                    ptr(tc), ntc, nfast_arg(L, nfc), ptr(st.Q), st.Q.stride(0), ptr(st.F),
+                    st.F.stride(0), ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2,
+                    ptr(rows), ptr(w), 100, tot, 1, ptr(qo), stream()),
+                100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel, qo)
+        if any(x.startswith("quant_fma_k300") for x in want):
+            # 300 VGG-16 clients (41 GB): launch pieces 3x as long as at K = 100, the
+            # per-piece fixed costs a third of the share
+            st3 = QuantizedClientStore(template, dev, capacity=300)
+            st3.Q.random_(0, 256, generator=g)
+            st3.F.normal_(generator=g)
+            st3.sz[..., 0].uniform_(1e-4, 1e-2, generator=g)
+            st3.sz[..., 1].zero_()
+            r3 = torch.arange(300, dtype=torch.int32, device=dev)
+            w3 = torch.randint(100, 1000, (300,), generator=g, device=dev).float()
+            t3 = float(w3.sum())
+            for cap in (None, 2048, 1024):
+                if cap is None:
+                    tc, ntc, nfc = st3.table(1)
+                    tag = ""
+                else:
+                    tc, ntc, nfc = capped_table(st3.qlayout, cap)
+                    tag = f"_t{cap // 1024}"
+                W["quant_fma_k300" + tag] = (
+                    lambda L, tc=tc, ntc=ntc, nfc=nfc: L.dls_dequant_fedavg_mode(
+                        ptr(tc), ntc, nfast_arg(L, nfc), ptr(st3.Q), st3.Q.stride(0), ptr(st3.F),
+                        st3.F.stride(0), ptr(st3.sz), st3.sz.stride(1) // 2,
+                        st3.sz.stride(0) // 2, ptr(r3), ptr(w3), 300, t3, 1, ptr(qo), stream()),
+                    300 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel, qo)
+        # the FMA table's one-channel 4 KiB group alone (group 0: the fc layers) and
+        # its lane groups alone: where the call's time goes
+        tfh = ql.tiles(qsv.LANE_TILE_FMA, one_channel=True)
+        toc, noc = ql.tiles(qsv.LANE_TILE_FMA, one_channel=True)  # the round-4 FMA table
+        tocd = torch.from_numpy(toc.view(np.uint8).copy()).to(dev)
+        W["quant_fma_oc"] = (lambda L: L.dls_dequant_fedavg_mode(
+            ptr(tocd), len(toc), nfast_arg(L, noc), ptr(st.Q), st.Q.stride(0), ptr(st.F),
+            st.F.stride(0), ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2, ptr(rows),
+            ptr(w), 100, tot, 1, ptr(qo), stream()),
+            100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel, qo)
+        tnew = ql.tiles(qsv.LANE_TILE_FMA, one_channel=False)
+        keep8 = qsv.LANE_TILE_MAX
+        qsv.LANE_TILE_MAX = 8192
+        t8, n8 = ql.tiles(qsv.LANE_TILE_FMA, one_channel=False)
+        qsv.LANE_TILE_MAX = keep8
+        t8d = torch.from_numpy(t8.view(np.uint8).copy()).to(dev)
+        W["quant_fma_w8"] = (lambda L: L.dls_dequant_fedavg_mode(
+            ptr(t8d), len(t8), nfast_arg(L, n8), ptr(st.Q), st.Q.stride(0), ptr(st.F),
+            st.F.stride(0), ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2, ptr(rows),
+            ptr(w), 100, tot, 1, ptr(qo), stream()),
+            100 * (Pq + 4 * Pf + 8 * ql.C) + 4 * st.layout.numel, qo)
+        for tag, lo, hi, tsrc in (("g0", 0, 1, tfh), ("lanes", 4, 8, tfh),
+                                  ("int", 0, 8, tnew)):
+            tt_, nf_ = tsrc
+            a0, a1 = sum(nf_[:lo]), sum(nf_[:hi])
+            sub = tt_[a0:a1]
+            nsub = tuple(nf_[g] if lo <= g < hi else 0 for g in range(len(nf_)))
+            td = torch.from_numpy(sub.view(np.uint8).copy()).to(dev)
+            nbs = 100 * int(sub["len"].sum()) + 4 * int(((sub["len"] + 63) // 64 * 64).sum())
+            W[f"quant_fma_{tag}"] = (
+                lambda L, td=td, sub=sub, nsub=nsub: L.dls_dequant_fedavg_mode(
+                    ptr(td), len(sub), nfast_arg(L, nsub), ptr(st.Q), st.Q.stride(0), ptr(st.F),
+                    st.F.stride(0), ptr(st.sz), st.sz.stride(1) // 2, st.sz.stride(0) // 2,
+                    ptr(rows), ptr(w), 100, tot, 1, ptr(qo), stream()), nbs, qo)
         rows0 = torch.zeros(100, dtype=torch.int32, device=dev)
         from distributed_learning_simulator_amd import quant_store as qs0
         for fwv in (0, 8, 16):
@@ -204,6 +280,16 @@ def setup(dev, want=()):
         W["quant_r18_a"] = (qmode(tab_a, r1k, w1k, t1k, 0), nb, qo18)
         # DLS_FEDAVG_FMA (1e-6 tolerance mode) on the same 1000 clients
         W["quant_r18_fma"] = (qmode(tab_f, r1k, w1k, t1k, 1), nb, qo18)
+        keep = qs.LANE_TILE_MAX
+        qs.LANE_TILE_MAX = 8192
+        W["quant_r18_fma_w8"] = (qmode(table(qs.LANE_TILE_FMA), r1k, w1k, t1k, 1), nb, qo18)
+        qs.LANE_TILE_MAX = keep
+        for cap in (3072, 2048, 1024):
+            keep = (qs.FAST_TILE, qs.LANE_TILE_MAX)
+            qs.FAST_TILE, qs.LANE_TILE_MAX = cap, cap
+            tab_c = table(qs.LANE_TILE_FMA)
+            qs.FAST_TILE, qs.LANE_TILE_MAX = keep
+            W[f"quant_r18_fma_t{cap // 1024}"] = (qmode(tab_c, r1k, w1k, t1k, 1), nb, qo18)
         # the previous adaptive rule (4 / 2 / 1 KiB by row length, rows < 336 to the
         # small-int tiles): the tile-width policy A/B on the same kernels
         keep_rule = qs._adaptive_lane_tile
@@ -302,6 +388,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--only-run", action="store_true", help="just launch (rocprofv3 target)")
+    ap.add_argument("--variants", default="",
+                    help="comma-separated variant names (default: every lib in the directory)")
     ap.add_argument("--check", action="store_true",
                     help="workloads that name their output: every variant's bits equal the first's")
     args = ap.parse_args()
@@ -311,6 +399,9 @@ def main():
             for p in sorted(glob.glob(os.path.join(
                 os.environ.get("DLS_VARIANTS", os.path.join(ROOT, "tools", "_variants")),
                 "libdls_*.so")))}
+    if args.variants:
+        keep = args.variants.split(",")
+        libs = {k: libs[k] for k in keep}
     W = setup(dev, args.workloads.split(","))
     res = {}
     for wl in args.workloads.split(","):
@@ -335,13 +426,19 @@ def main():
             torch.cuda.synchronize()
             print(wl, "ran", args.launches, flush=True)
             continue
-        times = {v: [] for v in libs}
-        for name, L in libs.items():  # warm (and check status)
+        # warm (and check status): a variant that refuses the workload (e.g. a build
+        # whose kernels do not take this table's tile widths) is skipped for it
+        run = {}
+        for name, L in libs.items():
             rc = fn(L)
-            assert rc == 0, (wl, name, rc, L.dls_last_error())
+            if rc != 0:
+                print(wl, "skip", name, rc, L.dls_last_error().decode(), flush=True)
+                continue
+            run[name] = L
         torch.cuda.synchronize()
+        times = {v: [] for v in run}
         for _ in range(args.rounds):
-            for name, L in libs.items():
+            for name, L in run.items():
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 for _ in range(args.launches):
@@ -349,7 +446,7 @@ def main():
                 b.record()
                 b.synchronize()
                 times[name].append(a.elapsed_time(b) / args.launches)
-        for name in libs:
+        for name in run:
             ms = statistics.median(times[name])
             res.setdefault(wl, {})[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1),
                                            "min_ms": round(min(times[name]), 4)}

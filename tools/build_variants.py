@@ -11,7 +11,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "distributed_learning_simulator_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "_variants")
-SRCS = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "shapley.hip", "infer.hip"]
+SRCS = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "quant_fma.hip", "shapley.hip",
+        "infer.hip"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off"]
 
 
@@ -23,6 +24,8 @@ def build(name, defs, src=CSRC):
     # objects of the others (the knob does not touch them)
     only = [x for x in os.environ.get("DLS_VARIANT_SRCS", "").split(",") if x]
     for s in SRCS:
+        if not os.path.exists(os.path.join(src, s)):  # a revision from before this source
+            continue
         o = os.path.join(d, s.replace(".hip", ".o"))
         if only and s not in only:
             o = os.path.join(CSRC, "_build", s.replace(".hip", ".o"))
@@ -50,8 +53,13 @@ def main(specs):
             os.makedirs(src, exist_ok=True)
             os.makedirs(os.path.join(tree, "include"), exist_ok=True)
             for f in SRCS + ["dls_common.h"]:
-                blob = subprocess.check_output(
-                    ["git", "-C", ROOT, "show", f"{rev}:distributed_learning_simulator_amd/csrc/{f}"])
+                try:
+                    blob = subprocess.check_output(
+                        ["git", "-C", ROOT, "show",
+                         f"{rev}:distributed_learning_simulator_amd/csrc/{f}"],
+                        stderr=subprocess.DEVNULL)
+                except subprocess.CalledProcessError:  # not in that revision
+                    continue
                 open(os.path.join(src, f), "wb").write(blob)
             blob = subprocess.check_output(["git", "-C", ROOT, "show", f"{rev}:include/dls_hip.h"])
             open(os.path.join(tree, "include", "dls_hip.h"), "wb").write(blob)
