@@ -44,12 +44,12 @@ hipStream_t side_stream(hipStream_t parent, int idx);
 // joins), created on first use and kept per (parent stream, idx), so a call
 // allocates nothing; nullptr on error.
 hipEvent_t call_event(hipStream_t parent, int idx);
-// FMA mode of dls_dequant_fedavg_mode: the int tiles of table groups 0-7 in
-// launch pieces of one wave per SIMD (quant_fma.hip).
+// FMA mode of dls_dequant_fedavg_mode: the tiles of table groups 0-9 in launch
+// pieces of one wave per SIMD (quant_fma.hip; groups 8-9 exact).
 int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, const void *Q,
-                              int64_t ldq, const float *sz, int64_t sz_row, int64_t sz_chan,
-                              const int32_t *rows, const float *w, int32_t K, float N, float *out,
-                              hipStream_t st);
+                              int64_t ldq, const float *F, int64_t ldf, const float *sz,
+                              int64_t sz_row, int64_t sz_chan, const int32_t *rows, const float *w,
+                              int32_t K, float N, float *out, hipStream_t st);
 
 inline hipStream_t as_stream(dls_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 inline bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }

@@ -39,9 +39,12 @@
 #include <type_traits>
 
 #include "dls_common.h"
+#include "quant_common.h"
 
 namespace dls {
 namespace {
+
+using namespace quant;
 
 constexpr int kFmaBlock = 256;  // 4 waves: a piece places one block per CU, one wave per SIMD
 constexpr int kFmaSpan = 4;     // channels per staged table (a tile over more: passes)
@@ -49,16 +52,18 @@ constexpr int kFmaSpan = 4;     // channels per staged table (a tile over more: 
 #ifndef DLS_FMA_D
 #define DLS_FMA_D 2
 #endif
-constexpr int kFmaD = DLS_FMA_D;  // clients in flight per wave (divides 64)
-static_assert(64 % kFmaD == 0, "the ring depth must divide the 64-client chunk");
+constexpr int kFmaD = DLS_FMA_D;  // clients in flight per wave
+static_assert(kFmaD >= 1 && kFmaD <= 64, "the ring depth");
 #ifndef DLS_FMA_GMAX
 #define DLS_FMA_GMAX 4
 #endif
 constexpr int kFmaGMax = DLS_FMA_GMAX;  // widest tile (KiB slices) the kernel instantiates
 #ifndef DLS_FMA_T
-#define DLS_FMA_T 1
+#define DLS_FMA_T 0
 #endif
-constexpr int kFmaT = DLS_FMA_T;  // tiles per wave per launch piece
+// tiles per wave per launch piece; 0: 2 for short client walks (K <= 256: the
+// pieces' fixed start and drain are a larger share of a 100-client walk), else 1
+constexpr int kFmaT = DLS_FMA_T;
 #ifndef DLS_FMA_WPS
 #define DLS_FMA_WPS 1
 #endif
@@ -70,18 +75,12 @@ constexpr int kFmaWps = DLS_FMA_WPS;  // waves per SIMD per launch piece
 #define DLS_FMA_PROBE 0  // 1: stream-only timing probe (loads + a xor per dword; wrong output)
 #endif
 
-struct SzL {
-    int64_t row, chan;  // (scale, zp) pair of (client row r, channel c) at r*row + c*chan
-};
-
 // The tile order: segment s (widest tiles first: table groups 0, 4, 1, 5, 2, 6,
 // 3, 7) holds indices [cum[s], cum[s+1]), table indices start[s] + i.
 struct FmaPlan {
     int cum[9];
     int start[8];
 };
-
-__device__ __forceinline__ int rl_i(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
 
 // Bytes HI*2, HI*2+1 of w as two fp32 values (sign-extended for int8: SDWA byte
 // select; unsigned: v_cvt_f32_ubyteN).  In volatile asm so that the conversions
@@ -147,7 +146,7 @@ struct FmaCall {
     const uint8_t *Q;
     int64_t ldq;
     const f32x2 *sz;
-    SzL L;
+    SzLayout L;
     const int32_t *rows;
     const float *w;
     int K;
@@ -178,10 +177,22 @@ __device__ __forceinline__ dls_qtile uniform_tile(const dls_qtile *p) {
 // walked over all K clients with D in flight.  rf0/wf0, rf1/wf1: the chunk
 // tables of clients 0-63 and 64-127 (call-wide, loaded once per wave).  buf: the
 // wave's 4 KiB of LDS (coefficient table while walking, store transpose at the end).
+// Clients in flight per wave for G KiB slices: kFmaD at 3-4 KiB, more for narrower
+// tiles (DLS_FMA_DN: about the same bytes in flight; 0: kFmaD at every width).  A
+// 1 KiB tile of a 1000-client walk at 2 in flight is a ~1,000 x latency chain
+// that outlasts the launch piece's 4 KiB tiles.
+#ifndef DLS_FMA_DN
+#define DLS_FMA_DN 1
+#endif
+template <int G>
+constexpr int ring_depth() {
+    return (DLS_FMA_DN == 0 || G >= 3) ? kFmaD : (G == 2 ? 2 * kFmaD : 4 * kFmaD);
+}
+
 template <int G, bool SIGNED>
 __device__ __forceinline__ void fma_tile(const dls_qtile &t, const FmaCall &a, int rf0, float wf0,
                                          int rf1, float wf1, float *buf) {
-    constexpr int D = kFmaD;
+    constexpr int D = ring_depth<G>();
     f32x2(*tab)[64] = reinterpret_cast<f32x2(*)[64]>(buf);  // [kFmaSpan + 1][64]
     const int lane = __lane_id();
     const int K = a.K;
@@ -232,30 +243,34 @@ __device__ __forceinline__ void fma_tile(const dls_qtile &t, const FmaCall &a, i
         for (int c = 0; c < kFmaSpan; ++c) szn[c] = a.sz[choff[c] + (int64_t)r0 * a.L.row];
         u32x4 slot[D][G];
 #pragma unroll
-        for (int u = 0; u < D; ++u) fetch(slot[u], rl_i(r0, u));  // lanes >= K hold row K-1
-        for (int k = 0; k < Kpad; k += D) {
-            if ((k & 63) == 0) {  // chunk start (wave-uniform)
-                if (k > 0) {
-                    r0 = r1;
-                    w0 = w1;
-                    r1 = r2;
-                    w1 = w2;
-                    const int kk = min(k + 128 + lane, K - 1);
-                    r2 = a.rows[kk];
-                    w2 = a.w[kk];
-                }
-                const bool live = lane < K - k;  // lanes past K: c = 0
-#pragma unroll
-                for (int c = 0; c < kFmaSpan; ++c)  // c = fl(fl(s * n_i) / N), IEEE division
-                    tab[c][lane] = live ? f32x2{(szn[c].x * w0) / a.N, -szn[c].y} : f32x2{0.f, 0.f};
-#pragma unroll
-                for (int c = 0; c < kFmaSpan; ++c)  // the next chunk's (its rows landed a chunk ago)
-                    szn[c] = a.sz[choff[c] + (int64_t)r1 * a.L.row];
+        for (int u = 0; u < D; ++u) fetch(slot[u], readlane_i(r0, u));  // lanes >= K hold row K-1
+        auto chunk_start = [&](int k) {  // wave-uniform
+            if (k > 0) {
+                r0 = r1;
+                w0 = w1;
+                r1 = r2;
+                w1 = w2;
+                const int kk = min(k + 128 + lane, K - 1);
+                r2 = a.rows[kk];
+                w2 = a.w[kk];
             }
-            const int cb = k & ~63;
+            const bool live = lane < K - k;  // lanes past K: c = 0
+#pragma unroll
+            for (int c = 0; c < kFmaSpan; ++c)  // c = fl(fl(s * n_i) / N), IEEE division
+                tab[c][lane] = live ? f32x2{(szn[c].x * w0) / a.N, -szn[c].y} : f32x2{0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < kFmaSpan; ++c)  // the next chunk's (its rows landed a chunk ago)
+                szn[c] = a.sz[choff[c] + (int64_t)r1 * a.L.row];
+        };
+        for (int k = 0; k < Kpad; k += D) {
+            if constexpr (64 % D == 0)
+                if ((k & 63) == 0) chunk_start(k);
 #pragma unroll
             for (int u = 0; u < D; ++u) {
-                const int j = (k + u) & 63;
+                const int kk = k + u;
+                if constexpr (64 % D != 0)
+                    if ((kk & 63) == 0) chunk_start(kk);
+                const int j = kk & 63;
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     if constexpr (DLS_FMA_PROBE == 1)
@@ -264,8 +279,8 @@ __device__ __forceinline__ void fma_tile(const dls_qtile &t, const FmaCall &a, i
                     else
                         fma16<SIGNED>(acc[g], slot[u][g], tab[0][toff[g] + j]);
                 }
-                const int f = k + u + D;  // < 64 (cb / 64 + 2): in chunk cb or the next
-                fetch(slot[u], f - cb < 64 ? rl_i(r0, f & 63) : rl_i(r1, f & 63));
+                const int f = kk + D, cb = kk & ~63;  // f < cb + 128: in chunk cb or the next
+                fetch(slot[u], f - cb < 64 ? readlane_i(r0, f & 63) : readlane_i(r1, f & 63));
             }
         }
     }
@@ -302,15 +317,39 @@ __device__ __forceinline__ void fma_tile(const dls_qtile &t, const FmaCall &a, i
     }
 }
 
+// The fp32 and small-int tiles of the call (table groups 8 and 9), walked by the
+// first launch piece's extra blocks with the exact arithmetic (quant_common.h):
+// no side streams, so no fork / join between calls (~20 us each).
+struct FmaSide {
+    const dls_qtile *f32;
+    int nf32;
+    const dls_qtile *small;
+    int nsmall;
+    const float *F;
+    int64_t ldf;
+    FastDiv d;
+    int main_blocks;  // blocks of the piece's main tiles; the side tiles' follow
+};
+
 // One launch piece: wave w of the piece walks tiles qbase + w + i * nwaves < qend
-// (one tile per wave at T = 1).
+// (T tiles per wave, the launcher sizes the piece so).
 __global__ __launch_bounds__(kFmaBlock) void k_dequant_fma_stream(const dls_qtile *__restrict__ tiles,
                                                                   FmaPlan plan, FmaCall a, int qbase,
-                                                                  int qend) {
+                                                                  int qend, FmaSide side) {
     __shared__ __attribute__((aligned(16))) float sbuf[kFmaBlock / 64][1024];
     float *buf = sbuf[threadIdx.x >> 6];
-    const int nwaves = (int)gridDim.x * (kFmaBlock / 64);
     const int lane = __lane_id();
+    if ((int)blockIdx.x >= side.main_blocks) {  // block-uniform
+        const int i = ((int)blockIdx.x - side.main_blocks) * (kFmaBlock / 64) + (int)(threadIdx.x >> 6);
+        __builtin_amdgcn_s_setprio(3);  // few long client walks beside the stream's waves
+        if (i < side.nf32)
+            f32_side_tile(side.f32[i], side.F, side.ldf, a.rows, a.w, a.K, side.d, a.out);
+        else if (i < side.nf32 + side.nsmall)
+            small_side_tile(side.small[i - side.nf32], a.Q, a.ldq, a.sz, a.L, a.rows, a.w, a.K,
+                            side.d, a.out);
+        return;
+    }
+    const int nwaves = side.main_blocks * (kFmaBlock / 64);
     // chunk tables of clients 0-63 and 64-127 (the same for every tile)
     const int rf0 = a.rows[min(lane, a.K - 1)];
     const float wf0 = a.w[min(lane, a.K - 1)];
@@ -345,9 +384,9 @@ __global__ __launch_bounds__(kFmaBlock) void k_dequant_fma_stream(const dls_qtil
 
 // Groups 0-7 of an FMA-mode call (quant.hip dls_dequant_fedavg_mode).
 int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, const void *Q,
-                              int64_t ldq, const float *sz, int64_t sz_row, int64_t sz_chan,
-                              const int32_t *rows, const float *w, int32_t K, float N, float *out,
-                              hipStream_t st) {
+                              int64_t ldq, const float *F, int64_t ldf, const float *sz,
+                              int64_t sz_row, int64_t sz_chan, const int32_t *rows, const float *w,
+                              int32_t K, float N, float *out, hipStream_t st) {
     static const int order[8] = {0, 4, 1, 5, 2, 6, 3, 7};  // widest tiles first
     int gstart[8];
     for (int g = 0, s = 0; g < 8; ++g) {
@@ -361,7 +400,10 @@ int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, cons
         plan.cum[s + 1] = plan.cum[s] + nfast[order[s]];
     }
     const int ntotal = plan.cum[8];
-    if (ntotal == 0) return DLS_OK;
+    FmaSide side{tiles + gstart[7] + nfast[7], nfast[8], tiles + gstart[7] + nfast[7] + nfast[8],
+                 nfast[9], F, ldf, make_fastdiv(N), 0};
+    const int nside = nfast[8] + nfast[9];
+    if (ntotal == 0 && nside == 0) return DLS_OK;
     for (int g = 0; g < 8; ++g)  // groups g % 4 hold tiles of 4 - g % 4 slices
         DLS_REQUIRE(nfast[g] == 0 || 4 - g % 4 <= kFmaGMax, DLS_EINVAL,
                     "dls_dequant_fedavg_mode: group %d tiles are wider than this build's %d KiB",
@@ -374,16 +416,20 @@ int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, cons
         (int64_t)resident_blocks(reinterpret_cast<const void *>(k_dequant_fma_stream), kFmaBlock, 0) *
             wpb,
         (int64_t)device_cus() * 4 * kFmaWps);
-    const int64_t cap = (int64_t)kFmaT * resident;
-    const int64_t npieces = (ntotal + cap - 1) / cap;
-    const int64_t per = (ntotal + npieces - 1) / npieces;
+    const int T = kFmaT > 0 ? kFmaT : (K <= 256 ? 2 : 1);
+    const int64_t cap = (int64_t)T * resident;
+    const int64_t npieces = std::max<int64_t>(1, (ntotal + cap - 1) / cap);
+    const int64_t per = std::max<int64_t>(1, (ntotal + npieces - 1) / npieces);
     FmaCall a{reinterpret_cast<const uint8_t *>(Q), ldq, reinterpret_cast<const f32x2 *>(sz),
-              SzL{sz_row, sz_chan}, rows, w, (int)K, N, out};
-    for (int64_t q0 = 0; q0 < ntotal; q0 += per) {
+              SzLayout{sz_row, sz_chan}, rows, w, (int)K, N, out};
+    const int side_blocks = (nside + wpb - 1) / wpb;  // with the first piece
+    for (int64_t q0 = 0; q0 < std::max(ntotal, 1); q0 += per) {
         const int m = (int)(ntotal - q0 < per ? ntotal - q0 : per);
-        const int64_t waves = std::min<int64_t>(resident, m);
-        hipLaunchKernelGGL(k_dequant_fma_stream, dim3((unsigned)((waves + wpb - 1) / wpb)),
-                           dim3(kFmaBlock), 0, st, tiles, plan, a, (int)q0, (int)q0 + m);
+        const int64_t waves = std::min<int64_t>(resident, (m + T - 1) / T);  // T tiles per wave
+        side.main_blocks = (int)((waves + wpb - 1) / wpb);
+        const int extra = q0 == 0 ? side_blocks : 0;
+        hipLaunchKernelGGL(k_dequant_fma_stream, dim3((unsigned)(side.main_blocks + extra)),
+                           dim3(kFmaBlock), 0, st, tiles, plan, a, (int)q0, (int)q0 + m, side);
     }
     return check_launch("dls_dequant_fedavg_mode (fma)");
 }

@@ -201,17 +201,17 @@ class QuantLayout:
                 rows.append((off + e, src + e, min(TILE, n - e), kind, cb + e // rl if kind else 0,
                              rl, e % rl if kind else 0, cend))
 
-        def one_channel(r):
+        def in_one_channel(r):
             return r[3] != 0 and r[6] + r[2] <= r[5]  # kind int, row_pos + len <= row_len
 
         def slices(r):
             return (r[2] + 63) // 64 * 64 // TILE + ((r[2] + 63) // 64 * 64 % TILE != 0)
 
-        fast = [[r for r in rows if one_channel(r) and slices(r) == g] for g in (4, 3, 2, 1)]
+        fast = [[r for r in rows if in_one_channel(r) and slices(r) == g] for g in (4, 3, 2, 1)]
         # group 4: lane tiles of 4 KiB slices or more (FMA tables: up to LANE_TILE_MAX)
         fast += [[r for r in lane_rows if min(slices(r), 4) == g] for g in (4, 3, 2, 1)]
         fast += [f32_rows, small_rows]
-        rest = [r for r in rows if not one_channel(r)]
+        rest = [r for r in rows if not in_one_channel(r)]
         assert all(r[2] <= TILE for r in rest)
         return (np.array([r for grp in fast for r in grp] + rest, dtype=QTILE_DTYPE),
                 tuple(len(grp) for grp in fast))

@@ -180,7 +180,6 @@ def _shapley_worker(rank, world, port, tag, metric_dir, outq):
     else:
         server, layout, U = _setup(case, ShardedMultiRoundShapleyValueServer,
                                    metric_dir=metric_dir)
-    assert server.parameters.store.U.is_cuda  # the HIP kernels, on the GPU
     np.random.seed(case["seed"])
     local = server.local_worker_ids
     for w in local:  # the initial broadcast
@@ -190,6 +189,7 @@ def _shapley_worker(rank, world, port, tag, metric_dir, outq):
         server.worker_data_queue.add_task((i, int(case["n"][i]), d))
     for w in local:
         server.worker_data_queue.get_result(consumer=w, timeout=300)
+    assert server.parameters.store.U.is_cuda  # the HIP kernels, on the GPU
     sv = {int(k): float(v) for k, v in server.shapley_values[1].items()}
     outq.put((rank, sv, [tuple(x) for x in server.evaluated_subsets]))
     dist.destroy_process_group()
@@ -203,7 +203,7 @@ def test_sharded_shapley_servers_two_ranks(tag, tmp_path):
     coalitions are dealt over the ranks and the utilities all-reduced.  Shapley
     values within 1e-12 of the reference's golden (BASELINE config 5 client
     counts), the union of the ranks' evaluated coalitions is the golden set (each
-    evaluated once), and multiround writes the reference's metric_1 bytes."""
+    evaluated once), and multiround's rank 0 writes the reference's metric_1 bytes."""
     case = next(c for c in G.shapley_large_cases() if c["tag"] == tag)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -215,7 +215,7 @@ def test_sharded_shapley_servers_two_ranks(tag, tmp_path):
              for r in range(2)]
     for p in procs:
         p.start()
-    outs = dict((r, (sv, ev)) for r, sv, ev in (q.get(timeout=600) for _ in range(2)))
+    outs = dict((r, (sv, ev)) for r, sv, ev in _collect(procs, q, 2, 200))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
@@ -227,9 +227,27 @@ def test_sharded_shapley_servers_two_ranks(tag, tmp_path):
     assert not set(ev0) & set(ev1)  # dealt, not duplicated
     assert len(ev0) + len(ev1) == case["n_evaluated"]
     assert set(ev0) | set(ev1) == set(case["evaluated"])
-    if case["metric_pickle"] is not None:
-        for d in dirs:
-            assert (d / "metric_1").read_bytes() == case["metric_pickle"]
+    if case["metric_pickle"] is not None:  # rank 0 writes the metric_<round> side file
+        assert (dirs[0] / "metric_1").read_bytes() == case["metric_pickle"]
+        assert not (dirs[1] / "metric_1").exists()
+
+
+def _collect(procs, q, n, timeout):
+    """n results from the queue; fails as soon as a process exits without one
+    (a child's exception would otherwise leave the parent waiting out the timeout)."""
+    import queue as _queue
+    import time as _time
+    out, t0 = [], _time.monotonic()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=2))
+            continue
+        except _queue.Empty:
+            pass
+        dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+        assert not dead, f"a worker process failed: exit codes {dead}"
+        assert _time.monotonic() - t0 < timeout, "workers timed out"
+    return out
 
 
 def _logits_worker(seed, outq):
@@ -257,7 +275,7 @@ def test_utility_bit_identical_across_processes():
         q = ctx.Queue()
         p = ctx.Process(target=_logits_worker, args=(7, q))
         p.start()
-        res.append(q.get(timeout=300))
+        res.extend(_collect([p], q, 1, 200))
         p.join(60)
         assert p.exitcode == 0
     (la, loss_a, acc_a), (lb, loss_b, acc_b) = res

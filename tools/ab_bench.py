@@ -256,12 +256,12 @@ def setup(dev, want=()):
             + 4 * sr.layout.numel
         saved = qs.LANE_TILE
 
-        def table(lane_tile, f32_tile=None, small_tile=None):
+        def table(lane_tile, f32_tile=None, small_tile=None, one_channel=True):
             keep = (qs.F32_TILE, qs.SMALL_TILE)
             qs.LANE_TILE = lane_tile
             qs.F32_TILE = f32_tile or keep[0]
             qs.SMALL_TILE = small_tile or keep[1]
-            tt, nft = qlr.tiles()
+            tt, nft = qlr.tiles(one_channel=one_channel)
             qs.LANE_TILE = saved
             qs.F32_TILE, qs.SMALL_TILE = keep
             return torch.from_numpy(tt.view(np.uint8).copy()).to(dev), tt, nft
@@ -273,7 +273,12 @@ def setup(dev, want=()):
                 sr.F.stride(0), ptr(sr.sz), sr.sz.stride(1) // 2, sr.sz.stride(0) // 2,
                 ptr(rows_t), ptr(w_t), rows_t.numel(), tot, mode, ptr(qo18), stream())
         # the store's tilings (exact: LANE_TILE, FMA: LANE_TILE_FMA), 1 KiB and adaptive
-        tab_p, tab_f = table(saved), table(qs.LANE_TILE_FMA)
+        tab_p, tab_f = table(saved), table(qs.LANE_TILE_FMA, one_channel=qs.FMA_ONE_CHANNEL)
+        # the FMA table's int groups alone (no fp32 / small-int side groups)
+        tdf_, ttf_, nff_ = tab_f  # (names unique in setup(): the lambdas bind late)
+        nint = sum(nff_[:8])
+        tab_i = (tdf_, ttf_[:nint], tuple(nff_[:8]) + (0,) * (len(nff_) - 8))
+        W["quant_r18_fma_int"] = (qmode(tab_i, r1k, w1k, t1k, 1), nb, qo18)
         tab_1, tab_a = table(1024), table("adaptive")
         W["quant_r18"] = (qmode(tab_p, r1k, w1k, t1k, 0), nb, qo18)
         W["quant_r18_l1"] = (qmode(tab_1, r1k, w1k, t1k, 0), nb, qo18)
