@@ -116,6 +116,7 @@ struct ChunkRows {
 // tensor keep 2 * kF32U client rows in flight instead of one dependent load per
 // client (with K = 1000 clients the unpipelined loop is a ~2 ms latency chain).
 constexpr int kF32U = 16;
+template <int U = kF32U>
 __device__ __forceinline__ void f32_side_tile(const dls_qtile &t, const float *__restrict__ F,
                                               int64_t ldf, const int32_t *__restrict__ rows,
                                               const float *__restrict__ w, int K, const FastDiv &d,
@@ -141,8 +142,8 @@ __device__ __forceinline__ void f32_side_tile(const dls_qtile &t, const float *_
         return q;
     };
     struct Batch {
-        f32x4 x[kF32U];
-        float wk[kF32U];
+        f32x4 x[U];
+        float wk[U];
     };
     ChunkRows cr;
     cr.init(rows, w, K);
@@ -155,15 +156,15 @@ __device__ __forceinline__ void f32_side_tile(const dls_qtile &t, const float *_
             x = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(src + r * ldf));
             wk = readlane_f(tw, j);
         };
-        chunk_pipeline<kF32U, Batch>(
+        chunk_pipeline<U, Batch>(
             min(64, K - base),
             [&](int j0, Batch &b) {
 #pragma unroll
-                for (int u = 0; u < kF32U; ++u) fetch(j0 + u, b.x[u], b.wk[u]);
+                for (int u = 0; u < U; ++u) fetch(j0 + u, b.x[u], b.wk[u]);
             },
             [&](const Batch &b) {
 #pragma unroll
-                for (int u = 0; u < kF32U; ++u) acc = acc + term(b.x[u], b.wk[u]);
+                for (int u = 0; u < U; ++u) acc = acc + term(b.x[u], b.wk[u]);
             },
             [&](int j) {
                 f32x4 x;

@@ -71,6 +71,12 @@ constexpr int kFmaWps = DLS_FMA_WPS;  // waves per SIMD per launch piece
 #ifndef DLS_FMA_NTSTORE
 #define DLS_FMA_NTSTORE 1  // non-temporal output stores (0: plain, A/B knob)
 #endif
+#ifndef DLS_FMA_SIDE_PRIO
+#define DLS_FMA_SIDE_PRIO 0  // issue priority of the fp32 / small-int side waves (3: +1 %)
+#endif
+#ifndef DLS_FMA_F32U
+#define DLS_FMA_F32U 16  // clients per batch of the fp32 side walk (two batches in flight)
+#endif
 #ifndef DLS_FMA_PROBE
 #define DLS_FMA_PROBE 0  // 1: stream-only timing probe (loads + a xor per dword; wrong output)
 #endif
@@ -341,9 +347,10 @@ __global__ __launch_bounds__(kFmaBlock) void k_dequant_fma_stream(const dls_qtil
     const int lane = __lane_id();
     if ((int)blockIdx.x >= side.main_blocks) {  // block-uniform
         const int i = ((int)blockIdx.x - side.main_blocks) * (kFmaBlock / 64) + (int)(threadIdx.x >> 6);
-        __builtin_amdgcn_s_setprio(3);  // few long client walks beside the stream's waves
+        __builtin_amdgcn_s_setprio(DLS_FMA_SIDE_PRIO);  // few long client walks beside the stream
         if (i < side.nf32)
-            f32_side_tile(side.f32[i], side.F, side.ldf, a.rows, a.w, a.K, side.d, a.out);
+            f32_side_tile<DLS_FMA_F32U>(side.f32[i], side.F, side.ldf, a.rows, a.w, a.K, side.d,
+                                        a.out);
         else if (i < side.nf32 + side.nsmall)
             small_side_tile(side.small[i - side.nf32], a.Q, a.ldq, a.sz, a.L, a.rows, a.w, a.K,
                             side.d, a.out);

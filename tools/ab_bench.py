@@ -321,6 +321,14 @@ def setup(dev, want=()):
         W["quant_r18_k5000"] = (qmode(tab_p, r5k, w5k, t5k, 0), nb5)
         W["quant_r18_k5000_fma"] = (qmode(tab_f, r5k, w5k, t5k, 1), nb5)
         W["quant_r18_k5000_l2"] = (qmode(tab_p, torch.zeros_like(r5k), w5k, t5k, 0), nb5)
+        # >= 10 ms lane-kernel dispatches (the clock quotient is validated there,
+        # MI355X_MICROARCH.md DVFS): the rows walked 15 times
+        r15k, w15k = r1k.repeat(15), w1k.repeat(15)
+        t15k = float(w15k.sum())
+        nb15 = 15 * (nb - 4 * sr.layout.numel) + 4 * sr.layout.numel
+        W["quant_r18_k15000"] = (qmode(tab_p, r15k, w15k, t15k, 0), nb15)
+        W["quant_r18_k15000_fma"] = (qmode(tab_p, r15k, w15k, t15k, 1), nb15)
+        W["quant_r18_k15000_l2"] = (qmode(tab_p, torch.zeros_like(r15k), w15k, t15k, 0), nb15)
         tt, nft = tab_p[1], tab_p[2]
         if any(w.startswith("quant_r18_slab") for w in want):
             # slab-major emulation: every Q tile gets its own slab of 1000 consecutive

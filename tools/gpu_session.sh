@@ -13,6 +13,7 @@
 #   bench[:<bench.py args>]      python bench.py (default --steps 20 --warmup 5)
 #   trace:<workloads>[:<launches>]  rocprofv3 --kernel-trace --stats of ab_bench --only-run
 #   pmc:<counters>:<workloads>   one rocprofv3 --pmc pass (counters comma-separated)
+#   pmcv:<variant>:<counters>:<workload>:<name>  one --pmc pass of one variant -> <name>.csv
 #   py:<script> [args]           python -u <script> [args]
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -70,7 +71,8 @@ for step in "$@"; do
         wl="${rest%%:*}"
         launches="${rest#*:}"
         [ "$launches" = "$rest" ] && launches=20
-        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$n" -o run -- \
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$n" \
+            -o run -- \
             python3 -u tools/ab_bench.py --workloads "$wl" --only-run --launches "$launches" \
             > "$log" 2>&1
         rc=$?
@@ -79,10 +81,27 @@ for step in "$@"; do
     pmc)
         ctr="${rest%%:*}"
         wl="${rest#*:}"
-        timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } -d "$OUT/pmc_$n" -o run -- \
+        timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$OUT/pmc_$n" -o run -- \
             python3 -u tools/ab_bench.py --workloads "$wl" --only-run --launches 5 > "$log" 2>&1
         rc=$?
         tail -3 "$log"
+        ;;
+    pmcv)
+        # pmcv:<variant>:<counters>:<workload>:<name>  one counter pass of ONE variant
+        # library, its counter rows kept as <name>.csv
+        var="${rest%%:*}"; r2="${rest#*:}"
+        ctr="${r2%%:*}"; r3="${r2#*:}"
+        wl="${r3%%:*}"; name="${r3#*:}"
+        lib="$(mktemp -d /tmp/dlsv.XXXXXX)"
+        cp "$ROOT/tools/_variants/libdls_$var.so" "$lib/"
+        DLS_VARIANTS="$lib" timeout -s KILL 300 rocprofv3 --pmc ${ctr//,/ } --output-format csv \
+            -d "$lib/p" -o run -- python3 -u tools/ab_bench.py --workloads "$wl" --only-run \
+            --launches 2 > "$log" 2>&1
+        rc=$?
+        f="$lib/p/run_counter_collection.csv"
+        [ -f "$f" ] && { head -1 "$f"; grep 'dls::' "$f" || true; } > "$OUT/$name.csv"
+        rm -rf "$lib"
+        tail -2 "$log"
         ;;
     py)
         # shellcheck disable=SC2086
