@@ -126,7 +126,7 @@ def _stream(stream=None, like=None):
 
 
 CSRC_HASHED = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "quant_fma.hip", "shapley.hip",
-               "infer.hip", "dls_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
+               "infer.hip", "dls_common.h", "quant_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
 
 
 def source_hash():
