@@ -77,6 +77,11 @@ SIGNATURES = {
     "dls_bn_fold_exact_f32": ([_p, _p, _p, _p, _f32, _i32, _p, _p], _i32),
     "dls_bn_act_exact_nhwc_f32": ([_p, _i64, _i32, _p, _p, _i32, _p, _p], _i32),
     "dls_bn_act_exact_nchw_f32": ([_p, _i64, _i32, _i64, _p, _p, _i32, _p, _p], _i32),
+    "dls_conv_pack_input_f32": ([_p, _i64, _i32, _i32, _i32, _i32, _p, _p], _i32),
+    "dls_conv_pack_weights_f32": ([_p, _i32, _i32, _i32, _i32, _i32, _p, _p], _i32),
+    "dls_conv_bn_act_split": ([_p, _i64, _i32, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _p,
+                               _i32, _p, _p], _i32),
+    "dls_pool_linear_split": ([_p, _i64, _i32, _i32, _p, _p, _i32, _p, _p], _i32),
 }
 
 _lib = None
@@ -126,7 +131,7 @@ def _stream(stream=None, like=None):
 
 
 CSRC_HASHED = ["dls_runtime.hip", "fedavg.hip", "sign.hip", "quant.hip", "quant_fma.hip", "shapley.hip",
-               "infer.hip", "dls_common.h", "quant_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
+               "infer.hip", "conv.hip", "dls_common.h", "quant_common.h", os.path.join("..", "..", "include", "dls_hip.h")]
 
 
 def source_hash():
@@ -353,3 +358,83 @@ def bn_act_exact(x, consts, residual=None, relu=True, out=None, inplace=False, s
     if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
         return bn_act_exact_nhwc(x, consts, residual, relu, out, inplace, stream)
     return bn_act_exact_nchw(x, consts, residual, relu, out, inplace, stream)
+
+
+# ------------------------------------------------ deterministic convolutions
+# "split" tensors (csrc/conv.hip): an fp32 value as a bf16 pair (hi, lo), stored
+# as int16 — activations [B, H, W, 2C] (per pixel C hi then C lo), weights
+# [Cout, 2K] (K hi then K lo, k = (ky*KW + kx)*Cp + ci).
+
+def split_channels(c):
+    """The padded channel count of a split tensor: a multiple of 32."""
+    return (int(c) + 31) // 32 * 32
+
+
+def conv_pack_input(x, stream=None):
+    """NCHW fp32 [B, C, H, W] -> split NHWC [B, H, W, 2 Cp] (zeros beyond C)."""
+    if x.dtype != torch.float32 or x.dim() != 4 or not x.is_contiguous():
+        raise RuntimeError("conv_pack_input: x must be a contiguous NCHW fp32 tensor")
+    B, C, H, W = x.shape
+    cp = split_channels(C)
+    out = torch.empty((B, H, W, 2 * cp), dtype=torch.int16, device=x.device)
+    _check(lib().dls_conv_pack_input_f32(_ptr(x), B, C, H, W, cp, _ptr(out), _stream(stream, x)),
+           "dls_conv_pack_input_f32")
+    return out
+
+
+def conv_pack_weights(w, stream=None):
+    """fp32 [Cout, Cin, KH, KW] -> split weights [Cout, 2K] with K = KH*KW*Cp."""
+    w = w.detach()
+    if w.dtype != torch.float32 or w.dim() != 4 or not w.is_contiguous():
+        raise RuntimeError("conv_pack_weights: w must be a contiguous fp32 [Cout, Cin, KH, KW]")
+    co, ci, kh, kw = w.shape
+    cp = split_channels(ci)
+    out = torch.empty((co, 2 * kh * kw * cp), dtype=torch.int16, device=w.device)
+    _check(lib().dls_conv_pack_weights_f32(_ptr(w), co, ci, kh, kw, cp, _ptr(out),
+                                           _stream(stream, w)), "dls_conv_pack_weights_f32")
+    return out
+
+
+def conv_bn_act(x, w, ksize, stride, pad, consts=None, residual=None, relu=True, out=None,
+                stream=None):
+    """y = act(bn(conv(x)) [+ residual]) over split NHWC activations
+    (dls_conv_bn_act_split); w from conv_pack_weights, ksize = (KH, KW)."""
+    B, H, W, c2 = x.shape
+    kh, kw = ksize
+    cout = w.shape[0]
+    ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    if x.dtype != torch.int16 or w.dtype != torch.int16 or not (x.is_contiguous() and w.is_contiguous()):
+        raise RuntimeError("conv_bn_act: split int16 contiguous operands expected")
+    if w.shape[1] != kh * kw * c2:
+        raise RuntimeError(f"conv_bn_act: weights {tuple(w.shape)} do not match input channels {c2 // 2}")
+    if residual is not None and (tuple(residual.shape) != (B, ho, wo, 2 * cout)
+                                 or not residual.is_contiguous()):
+        raise RuntimeError("conv_bn_act: residual must be split NHWC of the output's shape")
+    if out is None:
+        out = torch.empty((B, ho, wo, 2 * cout), dtype=torch.int16, device=x.device)
+    _check(lib().dls_conv_bn_act_split(_ptr(x), B, H, W, c2 // 2, _ptr(w), cout, kh, kw, stride,
+                                       pad, _ptr(consts), _ptr(residual), int(bool(relu)),
+                                       _ptr(out), _stream(stream, x)), "dls_conv_bn_act_split")
+    return out
+
+
+def pool_linear(x, weight, bias=None, stream=None):
+    """Global average pool + linear layer over a split NHWC activation -> fp32
+    logits [B, O] (dls_pool_linear_split)."""
+    B, H, W, c2 = x.shape
+    O = weight.shape[0]
+    if weight.shape[1] != c2 // 2 or not weight.is_contiguous():
+        raise RuntimeError("pool_linear: weight must be a contiguous [O, C] fp32 tensor")
+    out = torch.empty((B, O), dtype=torch.float32, device=x.device)
+    _check(lib().dls_pool_linear_split(_ptr(x), B, H * W, c2 // 2, _ptr(weight.detach()),
+                                       _ptr(None if bias is None else bias.detach()), O, _ptr(out),
+                                       _stream(stream, x)), "dls_pool_linear_split")
+    return out
+
+
+def split_to_f32(x):
+    """hi + lo of a split NHWC tensor as fp32 NCHW (test / debugging helper)."""
+    c = x.shape[-1] // 2
+    u = x.to(torch.int32) & 0xFFFF
+    f = (u << 16).view(torch.float32)
+    return (f[..., :c] + f[..., c:]).permute(0, 3, 1, 2).contiguous()

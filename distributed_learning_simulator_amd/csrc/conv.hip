@@ -1,0 +1,399 @@
+// Deterministic convolutions for the utility evaluation (SURVEY.md §8 row a-3:
+// FedServer.get_metric, servers/fed_server.py:26-32 — the Shapley servers'
+// v(S) = top-1 accuracy of the subset model on the test set).
+//
+// Why our own: v(S) must be a function of S (GTG's truncation tests and the
+// rankings compare utilities, and on several ranks a coalition's utility must
+// not depend on which rank evaluated it).  MIOpen's fast convolutions are not
+// run-to-run reproducible on this stack, and its deterministic ones are NCHW
+// Winograd kernels (the Inferencer's round-4 path, ~7.4 evals/s).  These
+// kernels are reproducible by construction: every output element is reduced by
+// one wave in one fixed order (no split-K, no atomics, no algorithm search).
+//
+// Arithmetic: fp32 activations and weights, each carried as a pair of bf16
+// (hi = rne(x), lo = rne(x - hi): 16 significant bits), and every product taken
+// as hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation
+// ("bf16x3"): a relative error per product of ~2^-16 against fp32's 2^-24, at 3
+// bf16 MFMAs = 3/16 of the time of the f32-input MFMA (which runs at the fp32
+// vector rate, 157 TF: a ResNet-18 eval of 10k CIFAR images is 11.1 TFLOP,
+// >= 70 ms on it at peak).  The logits differ from torch's fp32 forward in the
+// low bits; top-1 agrees except where the top two logits are within that error
+// (tests/test_gpu_conv.py).
+//
+// Layouts (HBM):
+//   activations  "split NHWC": uint16 [B][H][W][2C], per pixel C bf16 hi then C
+//                bf16 lo (4 B per element, the size of the fp32 tensor);
+//   weights      uint16 [Cout][2K], per output channel K hi then K lo,
+//                k = (ky * KW + kx) * C + ci (C = the input's padded channels).
+// Implicit GEMM, D[co][pixel] = sum_k W[co][k] X[k][pixel]: A = weights (rows =
+// output channels), B = the input pixels' channel runs, gathered per tap (zero
+// outside the image); so a lane's 16-element MFMA fragment is one 16-B piece of
+// a pixel's hi (or lo) channel run.  Each block stages A and B chunks of BK
+// channels of one tap through double-buffered LDS (register staging, rows padded
+// by 16 B: conflict-free ds_read_b128 fragments), each wave owns a 64 x 64
+// (channel x pixel) output tile = 2 x 2 MFMA tiles.  The epilogue applies the
+// eval batch norm with the batch-norm library's arithmetic (infer.hip,
+// k_bn_act_exact: fma(w, (x - mean) * iv, b)), the residual add and the ReLU,
+// and stores the output split — the next convolution's operand — so a ResNet
+// block is 2 (or 3) launches and no separate batch-norm pass.
+#include "dls_common.h"
+
+namespace dls {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    const uint32_t u = __float_as_uint(x);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;  // NaN stays a (quiet) NaN
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// x = hi + lo + O(2^-17 |x|); lo = 0 for non-finite x (hi carries the inf / NaN)
+__device__ __forceinline__ void split2(float x, uint32_t &hi, uint32_t &lo) {
+    hi = bf16_rne(x);
+    const float r = x - __uint_as_float(hi << 16);
+    lo = (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u ? 0u : bf16_rne(r);
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+struct ConvArgs {
+    const uint16_t *x;      // split NHWC input [B][H][W][2C]
+    const uint16_t *w;      // split weights [Cout][2K]
+    const float *consts;    // eval batch norm [mean | iv | w | b] x Cout, or null
+    const uint16_t *res;    // split residual [B][Ho][Wo][2 Cout], or null
+    uint16_t *y;            // split output [B][Ho][Wo][2 Cout]
+    int H, W, C, Ho, Wo, Cout, KW, taps, stride, pad, K, M, relu;
+    int pix_tiles, co_tiles;
+};
+
+constexpr int kWaveTile = 64;  // a wave's output tile: 64 channels x 64 pixels
+
+template <int BK, int WCO, int WPIX>
+__global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
+    constexpr int NT = 64 * WCO * WPIX;
+    constexpr int BMC = kWaveTile * WCO;   // output channels per block
+    constexpr int BNP = kWaveTile * WPIX;  // pixels per block
+    constexpr int ROWB = 4 * BK + 16;      // LDS row: BK hi, BK lo (bf16), 16 B pad
+    constexpr int PPR = BK / 4;            // 16-B pieces per row
+    constexpr int HP = BK / 8;             // of which hi
+    constexpr int RPP = NT / PPR;          // rows per staging pass
+    constexpr int NA = BMC / RPP, NB = BNP / RPP;
+    static_assert(NT % PPR == 0 && BMC % RPP == 0 && BNP % RPP == 0, "staging shape");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (BMC + BNP) * ROWB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wc = wid / WPIX, wp = wid % WPIX;
+    // XCD-aware tile order: the 8 XCDs take consecutive blockIdx round-robin;
+    // give each a contiguous run of (pixel tile, channel tile) pairs, channel tile
+    // fastest, so blocks reading the same input pixels share an L2
+    const int nblk = gridDim.x;
+    const int bid = blockIdx.x;
+    int t = bid;
+    if ((nblk & 7) == 0) t = (bid & 7) * (nblk >> 3) + (bid >> 3);
+    const int co0 = (t % a.co_tiles) * BMC;
+    const int pix0 = (t / a.co_tiles) * BNP;
+
+    // staging assignment: piece `part` of rows tid / PPR + RPP * u
+    const int part = tid % PPR, row0 = tid / PPR;
+    const int poff = part < HP ? part * 8 : BK + (part - HP) * 8;  // element offset in a chunk
+    int pbase[NB], piy[NB], pix_[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int p = pix0 + row0 + RPP * u;
+        if (p < a.M) {
+            const int hw = a.Ho * a.Wo;
+            const int b = p / hw, rem = p - b * hw;
+            const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+            pbase[u] = b * a.H * a.W;
+            piy[u] = oy * a.stride - a.pad;
+            pix_[u] = ox * a.stride - a.pad;
+        } else {
+            pbase[u] = 0;
+            piy[u] = -(1 << 20);  // never inside the image: loads zero
+            pix_[u] = 0;
+        }
+    }
+    const uint16_t *wrow[NA];
+#pragma unroll
+    for (int u = 0; u < NA; ++u) wrow[u] = a.w + (int64_t)(co0 + row0 + RPP * u) * (2 * a.K);
+
+    const int cchunks = a.C / BK;
+    const int nchunks = a.taps * cchunks;
+    u32x4 ra[NA], rb[NB];
+    auto load = [&](int c) {
+        const int tap = c / cchunks, ci0 = (c - tap * cchunks) * BK;
+        const int ky = tap / a.KW, kx = tap - ky * a.KW;
+        const int kc = tap * a.C + ci0;
+        const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
+#pragma unroll
+        for (int u = 0; u < NA; ++u) ra[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
+        const int xo = part < HP ? ci0 + part * 8 : a.C + ci0 + (part - HP) * 8;
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int iy = piy[u] + ky, ix = pix_[u] + kx;
+            if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
+                const int64_t pe = (int64_t)(pbase[u] + iy * a.W + ix) * (2 * a.C) + xo;
+                rb[u] = *reinterpret_cast<const u32x4 *>(a.x + pe);
+            } else {
+                rb[u] = u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+    };
+    auto store = [&](int buf) {
+        uint8_t *As = smem + buf * (BMC + BNP) * ROWB;
+        uint8_t *Bs = As + BMC * ROWB;
+#pragma unroll
+        for (int u = 0; u < NA; ++u)
+            *reinterpret_cast<u32x4 *>(As + (row0 + RPP * u) * ROWB + poff * 2) = ra[u];
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+            *reinterpret_cast<u32x4 *>(Bs + (row0 + RPP * u) * ROWB + poff * 2) = rb[u];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int r = lane & 31, h = lane >> 5;
+    auto compute = [&](int buf) {
+        const uint8_t *As = smem + buf * (BMC + BNP) * ROWB + (wc * kWaveTile + r) * ROWB;
+        const uint8_t *Bs = smem + buf * (BMC + BNP) * ROWB + (BMC + wp * kWaveTile + r) * ROWB;
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {
+            const int off = 32 * s + 16 * h;  // bytes: k = 16 s + 8 h .. + 7
+            bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ah[i] = *reinterpret_cast<const bf16x8 *>(As + i * 32 * ROWB + off);
+                al[i] = *reinterpret_cast<const bf16x8 *>(As + i * 32 * ROWB + 2 * BK + off);
+                bh[i] = *reinterpret_cast<const bf16x8 *>(Bs + i * 32 * ROWB + off);
+                bl[i] = *reinterpret_cast<const bf16x8 *>(Bs + i * 32 * ROWB + 2 * BK + off);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+    };
+
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+        const bool more = c + 1 < nchunks;
+        if (more) load(c + 1);
+        compute(c & 1);
+        if (more) store((c + 1) & 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane holds pixel pix0 + wp*64 + 32 j + r, channels
+    // co0 + wc*64 + 32 i + 8 g + 4 h + e  (e < 4) in acc[i][j][4 g + e]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int p = pix0 + wp * kWaveTile + 32 * j + r;
+        if (p >= a.M) continue;
+        const int64_t ob = (int64_t)p * (2 * a.Cout);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int co = co0 + wc * kWaveTile + 32 * i + 8 * g + 4 * h;
+                f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                           acc[i][j][4 * g + 3]};
+                if (a.consts) {
+                    const f32x4 m = *reinterpret_cast<const f32x4 *>(a.consts + co);
+                    const f32x4 iv = *reinterpret_cast<const f32x4 *>(a.consts + a.Cout + co);
+                    const f32x4 wv = *reinterpret_cast<const f32x4 *>(a.consts + 2 * a.Cout + co);
+                    const f32x4 bv = *reinterpret_cast<const f32x4 *>(a.consts + 3 * a.Cout + co);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
+                }
+                if (a.res) {
+                    const u32x2 rh = *reinterpret_cast<const u32x2 *>(a.res + ob + co);
+                    const u32x2 rl = *reinterpret_cast<const u32x2 *>(a.res + ob + a.Cout + co);
+                    v[0] = v[0] + (bf16_to_f32(rh[0] & 0xffffu) + bf16_to_f32(rl[0] & 0xffffu));
+                    v[1] = v[1] + (bf16_to_f32(rh[0] >> 16) + bf16_to_f32(rl[0] >> 16));
+                    v[2] = v[2] + (bf16_to_f32(rh[1] & 0xffffu) + bf16_to_f32(rl[1] & 0xffffu));
+                    v[3] = v[3] + (bf16_to_f32(rh[1] >> 16) + bf16_to_f32(rl[1] >> 16));
+                }
+                uint32_t hi[4], lo[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = v[e];
+                    if (a.relu) x = x > 0.f ? x : (x == x ? 0.f : x);  // relu keeps NaN, as torch
+                    split2(x, hi[e], lo[e]);
+                }
+                *reinterpret_cast<u32x2 *>(a.y + ob + co) = u32x2{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16)};
+                *reinterpret_cast<u32x2 *>(a.y + ob + a.Cout + co) =
+                    u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+            }
+    }
+}
+
+// fp32 NCHW image batch -> split NHWC with Cp >= C channels (zeros beyond C)
+__global__ __launch_bounds__(256) void k_pack_input(const float *__restrict__ x, int64_t n, int C,
+                                                   int HW, int Cp, uint16_t *__restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, ci) with ci fastest
+    if (i >= n) return;
+    const int ci = (int)(i % Cp);
+    const int64_t pix = i / Cp;
+    const int64_t b = pix / HW, s = pix - b * HW;
+    const float v = ci < C ? x[(b * C + ci) * HW + s] : 0.f;
+    uint32_t hi, lo;
+    split2(v, hi, lo);
+    y[pix * 2 * Cp + ci] = (uint16_t)hi;
+    y[pix * 2 * Cp + Cp + ci] = (uint16_t)lo;
+}
+
+// fp32 [Cout][Cin][KH][KW] -> split [Cout][2K], k = (ky * KW + kx) * Cp + ci
+__global__ __launch_bounds__(256) void k_pack_weights(const float *__restrict__ w, int Cout, int Cin,
+                                                     int KH, int KW, int Cp, uint16_t *__restrict__ y) {
+    const int K = KH * KW * Cp;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)Cout * K) return;
+    const int co = (int)(i / K), k = (int)(i - (int64_t)co * K);
+    const int tap = k / Cp, ci = k - tap * Cp;
+    const int ky = tap / KW, kx = tap - ky * KW;
+    const float v = ci < Cin ? w[(((int64_t)co * Cin + ci) * KH + ky) * KW + kx] : 0.f;
+    uint32_t hi, lo;
+    split2(v, hi, lo);
+    y[(int64_t)co * 2 * K + k] = (uint16_t)hi;
+    y[(int64_t)co * 2 * K + K + k] = (uint16_t)lo;
+}
+
+// Global average pool + linear layer over split NHWC [B][HW][2C]: one block per
+// image, every sum in one fixed order (per channel: pixels in order; per output:
+// a fixed tree over the block) -> logits [B][O] fp32.
+constexpr int kPoolBlock = 256;
+__global__ __launch_bounds__(kPoolBlock) void k_pool_linear(const uint16_t *__restrict__ x, int HW, int C,
+                                                            const float *__restrict__ wt,
+                                                            const float *__restrict__ bias, int O,
+                                                            float *__restrict__ out) {
+    __shared__ float red[kPoolBlock];
+    __shared__ float feat[2048];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const uint16_t *xb = x + (int64_t)b * HW * 2 * C;
+    const float inv = 1.f / (float)HW;
+    for (int c = tid; c < C; c += kPoolBlock) {
+        float s = 0.f;
+        for (int q = 0; q < HW; ++q)
+            s += bf16_to_f32(xb[(int64_t)q * 2 * C + c]) + bf16_to_f32(xb[(int64_t)q * 2 * C + C + c]);
+        feat[c] = s * inv;
+    }
+    __syncthreads();
+    for (int o = 0; o < O; ++o) {
+        float s = 0.f;
+        for (int c = tid; c < C; c += kPoolBlock) s = __builtin_fmaf(feat[c], wt[(int64_t)o * C + c], s);
+        red[tid] = s;
+        __syncthreads();
+        for (int k = kPoolBlock / 2; k > 0; k >>= 1) {
+            if (tid < k) red[tid] += red[tid + k];
+            __syncthreads();
+        }
+        if (tid == 0) out[(int64_t)b * O + o] = red[0] + (bias ? bias[o] : 0.f);
+        __syncthreads();
+    }
+}
+
+template <int BK, int WCO, int WPIX>
+int launch_conv(const ConvArgs &a0, hipStream_t st) {
+    ConvArgs a = a0;
+    a.pix_tiles = (a.M + kWaveTile * WPIX - 1) / (kWaveTile * WPIX);
+    a.co_tiles = a.Cout / (kWaveTile * WCO);
+    const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
+    if (blocks > INT32_MAX) {
+        set_error("dls_conv_bn_act_split: %lld blocks", (long long)blocks);
+        return DLS_EINVAL;
+    }
+    hipLaunchKernelGGL((k_conv_bf16x3<BK, WCO, WPIX>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
+                       st, a);
+    return check_launch("dls_conv_bn_act_split");
+}
+
+}  // namespace
+}  // namespace dls
+
+using namespace dls;
+
+extern "C" {
+
+int dls_conv_pack_input_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, int32_t Cp,
+                            uint16_t *out, dls_stream_t stream) {
+    DLS_REQUIRE(x && out, DLS_EINVAL, "dls_conv_pack_input_f32: null pointer");
+    DLS_REQUIRE(B >= 0 && C > 0 && H > 0 && W > 0 && Cp >= C && Cp % 32 == 0, DLS_EINVAL,
+                "dls_conv_pack_input_f32: B=%lld C=%d H=%d W=%d Cp=%d (Cp >= C, a multiple of 32)",
+                (long long)B, C, H, W, Cp);
+    const int64_t n = B * H * W * (int64_t)Cp;
+    if (n == 0) return DLS_OK;
+    hipLaunchKernelGGL(k_pack_input, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       x, n, (int)C, (int)(H * W), (int)Cp, out);
+    return check_launch("dls_conv_pack_input_f32");
+}
+
+int dls_conv_pack_weights_f32(const float *w, int32_t Cout, int32_t Cin, int32_t KH, int32_t KW,
+                              int32_t Cp, uint16_t *out, dls_stream_t stream) {
+    DLS_REQUIRE(w && out, DLS_EINVAL, "dls_conv_pack_weights_f32: null pointer");
+    DLS_REQUIRE(Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && Cp >= Cin && Cp % 32 == 0 &&
+                    (int64_t)KH * KW * Cp <= (1 << 24),
+                DLS_EINVAL, "dls_conv_pack_weights_f32: Cout=%d Cin=%d KH=%d KW=%d Cp=%d", Cout, Cin,
+                KH, KW, Cp);
+    const int64_t n = (int64_t)Cout * KH * KW * Cp;
+    hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), w, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Cp, out);
+    return check_launch("dls_conv_pack_weights_f32");
+}
+
+int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, int32_t C,
+                          const uint16_t *w, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                          int32_t pad, const float *consts, const uint16_t *residual, int32_t relu,
+                          uint16_t *y, dls_stream_t stream) {
+    DLS_REQUIRE(x && w && y, DLS_EINVAL, "dls_conv_bn_act_split: null pointer");
+    DLS_REQUIRE(B >= 0 && H > 0 && W > 0 && C >= 32 && C % 32 == 0 && Cout >= 64 && Cout % 64 == 0 &&
+                    KH > 0 && KW > 0 && stride > 0 && pad >= 0 && H + 2 * pad >= KH &&
+                    W + 2 * pad >= KW && (int64_t)KH * KW * C <= (1 << 24),
+                DLS_EINVAL,
+                "dls_conv_bn_act_split: B=%lld H=%d W=%d C=%d Cout=%d KH=%d KW=%d stride=%d pad=%d "
+                "(C a multiple of 32, Cout of 64)",
+                (long long)B, H, W, C, Cout, KH, KW, stride, pad);
+    DLS_REQUIRE(aligned16(x) && aligned16(w) && aligned16(y) && (!consts || aligned16(consts)) &&
+                    (!residual || aligned16(residual)),
+                DLS_ELAYOUT, "dls_conv_bn_act_split: 16-byte alignment");
+    const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+    const int64_t M = B * Ho * Wo;
+    if (M == 0) return DLS_OK;
+    // pixel indices are 32-bit inside the kernel; element offsets 64-bit
+    DLS_REQUIRE(M <= INT32_MAX / 2 && B * H * W <= INT32_MAX / 2, DLS_EINVAL,
+                "dls_conv_bn_act_split: %lld output pixels", (long long)M);
+    ConvArgs a{x, w, consts, residual, y, (int)H, (int)W, (int)C, Ho, Wo, (int)Cout, (int)KW,
+               (int)(KH * KW), (int)stride, (int)pad, (int)(KH * KW * C), (int)M, relu ? 1 : 0, 0, 0};
+    hipStream_t st = as_stream(stream);
+    if (Cout % 128 == 0) return launch_conv<32, 2, 2>(a, st);
+    return launch_conv<32, 1, 4>(a, st);
+}
+
+int dls_pool_linear_split(const uint16_t *x, int64_t B, int32_t HW, int32_t C, const float *weight,
+                          const float *bias, int32_t O, float *out, dls_stream_t stream) {
+    DLS_REQUIRE(x && weight && out, DLS_EINVAL, "dls_pool_linear_split: null pointer");
+    DLS_REQUIRE(B >= 0 && HW > 0 && C > 0 && C <= 2048 && O > 0, DLS_EINVAL,
+                "dls_pool_linear_split: B=%lld HW=%d C=%d O=%d (C <= 2048)", (long long)B, HW, C, O);
+    if (B == 0) return DLS_OK;
+    hipLaunchKernelGGL(k_pool_linear, dim3((unsigned)B), dim3(kPoolBlock), 0, as_stream(stream), x,
+                       (int)HW, (int)C, weight, bias, (int)O, out);
+    return check_launch("dls_pool_linear_split");
+}
+
+}  // extern "C"

@@ -97,6 +97,44 @@ class ResNet18(nn.Module):
                 fold[id(m)] = c
         return fold
 
+    @torch.no_grad()
+    def pack_split(self):
+        """The operands of forward_split: {id(conv): split weights} and {id(bn):
+        exact eval batch-norm consts} (recomputed per evaluation: the weights
+        change with the coalition)."""
+        from . import _native
+        pk = {}
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                if m.bias is not None or m.groups != 1 or m.dilation != (1, 1):
+                    raise RuntimeError("forward_split: plain bias-free convolutions only")
+                pk[id(m)] = _native.conv_pack_weights(m.weight.contiguous())
+            elif isinstance(m, nn.BatchNorm2d):
+                c = torch.empty(4 * m.num_features, device=m.running_mean.device)
+                _native.bn_fold_exact(m, c)
+                pk[id(m)] = c
+        return pk
+
+    def forward_split(self, x, pk):
+        """forward() for the utility evaluation on the GPU with the library's
+        deterministic convolutions (csrc/conv.hip): every conv + eval batch norm
+        (+ residual add) + ReLU one launch over split NHWC activations, then the
+        pooled linear layer; the same bits for the same model and input in any
+        process.  x: NCHW fp32 [B, 3, H, W]; pk = pack_split()."""
+        from . import _native
+
+        def cba(inp, conv, bn, residual=None, relu=True):
+            return _native.conv_bn_act(inp, pk[id(conv)], conv.kernel_size, conv.stride[0],
+                                       conv.padding[0], pk[id(bn)], residual, relu)
+
+        out = cba(_native.conv_pack_input(x.contiguous()), self.conv1, self.bn1)
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                h = cba(out, blk.conv1, blk.bn1)
+                sc = cba(out, blk.shortcut[0], blk.shortcut[1], relu=False) if len(blk.shortcut) else out
+                out = cba(h, blk.conv2, blk.bn2, residual=sc)
+        return _native.pool_linear(out, self.linear.weight, self.linear.bias)
+
     def forward_fused(self, x, fold):
         """forward() for utility evaluation on the GPU: NHWC or NCHW activations,
         MIOpen convolutions, every batch norm + ReLU (+ residual add) fused into one

@@ -78,35 +78,41 @@ class Inferencer:
     The utility of a coalition must be a function of the coalition: GTG's
     truncation tests (servers/GTG_shapley_value_server.py:29,54) and the client
     ranking compare utilities, and on several GPUs a coalition's utility must not
-    depend on which rank evaluated it.  MIOpen's default convolution algorithms
-    are not run-to-run reproducible on this stack (the 512-channel layers of
-    ResNet-18 gave different bits for the same input), so the GPU forward runs
-    with ``torch.backends.cudnn.deterministic = True, benchmark = False``
-    (``deterministic``, default on): MIOpen then only selects deterministic
-    convolution solutions.  Those are torch's process-wide switches, set for the
-    duration of ``inference()`` / ``logits()`` and restored after it (worker
-    threads that train meanwhile also get deterministic convolutions; their
-    results stay correct).  MIOpen's deterministic solutions are NCHW ones: on
-    channels_last activations it falls back to a naive kernel (~19 s instead of
-    0.2 s per 10k CIFAR images, profiles/r04q_eval_det.txt), so the reproducible
-    path keeps activations NCHW; ``deterministic=False`` runs channels_last
-    (NHWC), the faster layout for MIOpen's default algorithms.
+    depend on which rank evaluated it.
 
-    Models that have a ``forward_fused`` eval path (models.ResNet18) run it on the
-    GPU (``fused_eval``, default on): every batch norm + ReLU (+ residual add) as
-    one hand-written NHWC pass (dls_bn_act_exact_nhwc_f32) that reproduces the
-    eval batch norm torch runs on this stack (MIOpen's inference kernel); with
-    deterministic convolutions the logits are bit-identical to the module's
-    forward (tests/test_gpu_infer.py).  That equality is a property of this
-    torch / MIOpen build, so every Inferencer checks it once, on its model's
-    first batch norm against ``bn(x)``; if the bits differ it runs the module's
-    forward instead.  ``fused_eval=False`` always runs the module's forward."""
+    Models with a ``forward_split`` eval path (models.ResNet18) run it on the GPU
+    (``conv="dls"``, the default, with ``fused_eval``): the library's own
+    convolutions (csrc/conv.hip), each fused with its eval batch norm, residual
+    add and ReLU, reduced in one fixed order — the same bits for the same model
+    and input in any process, with no algorithm search and no process-wide
+    switches.  Their products are bf16x3 (fp32 values as bf16 pairs): the logits
+    differ from the module's fp32 forward in the low bits, top-1 only at near-ties
+    (tests/test_gpu_conv.py).
+
+    ``conv="miopen"`` runs torch / MIOpen convolutions instead.  MIOpen's default
+    algorithms are not run-to-run reproducible on this stack (the 512-channel
+    layers of ResNet-18 gave different bits for the same input), so that path
+    runs with ``torch.backends.cudnn.deterministic = True, benchmark = False``
+    (``deterministic``, default on) for the duration of ``inference()`` /
+    ``logits()``: torch's process-wide switches, restored after it.  MIOpen's
+    deterministic solutions are NCHW ones (on channels_last it falls back to a
+    naive kernel, ~19 s per 10k CIFAR images, profiles/r04q_eval_det.txt), so that
+    path keeps activations NCHW; ``deterministic=False`` runs channels_last.
+    There, models with a ``forward_fused`` eval path run every batch norm + ReLU
+    (+ residual add) as one hand-written pass (dls_bn_act_exact_*_f32) with
+    MIOpen's own batch-norm arithmetic: logits bit-identical to the module's
+    forward, checked once per Inferencer on its first batch norm (if the bits
+    differ it runs the module's forward).  ``fused_eval=False`` always runs the
+    module's forward."""
 
     def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True,
-                 deterministic=True):
+                 deterministic=True, conv="dls"):
+        if conv not in ("dls", "miopen"):
+            raise ValueError(f"Inferencer: conv must be 'dls' or 'miopen', not {conv!r}")
         self.model = model
         self.fused_eval = fused_eval
         self.deterministic = deterministic
+        self.conv = conv
         self.dataset = dataset
         self.batch_size = batch_size
         self.device = device or next(model.parameters()).device
@@ -118,8 +124,16 @@ class Inferencer:
         self.device = torch.device(device)
         self.model.to(self.device)
 
+    def _split_forward(self):
+        """model.forward_split when this Inferencer runs the library's convolutions."""
+        if not (self.fused_eval and self.conv == "dls" and self.dataset[0].dim() == 4
+                and torch.device(self.device).type == "cuda"):
+            return None
+        return getattr(self.model, "forward_split", None)
+
     def _flags(self):
-        if not self.deterministic or torch.device(self.device).type != "cuda":
+        if (not self.deterministic or torch.device(self.device).type != "cuda"
+                or self._split_forward() is not None):
             return contextlib.nullcontext()
         return _deterministic_convs()
 
@@ -166,6 +180,14 @@ class Inferencer:
         """Logits of every batch, in order (the model in eval mode)."""
         X, y = self.dataset
         self.model.eval()
+        split = self._split_forward()
+        if split is not None:
+            pk = self.model.pack_split()
+            for i in range(0, X.shape[0], self.batch_size):
+                xb = X[i:i + self.batch_size].to(self.device, torch.float32, non_blocking=True)
+                yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
+                yield split(xb.contiguous(), pk), yb
+            return
         fmt = self._memory_format()
         if X.dim() == 4 and torch.device(self.device).type == "cuda":
             # NHWC convolutions: measured 8-18 % faster than NCHW for this model family

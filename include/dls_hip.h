@@ -279,6 +279,35 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
                               const float *consts, const float *residual, int32_t relu, float *y,
                               dls_stream_t stream);
 
+/* Deterministic convolutions of the utility evaluation (replace the tester's
+ * torch / MIOpen conv2d in the model forward behind servers/fed_server.py:26-32;
+ * csrc/conv.hip).  Every output is reduced in one fixed order by one wave: the
+ * same inputs give the same bits in any process.  fp32 values are carried as
+ * bf16 pairs (hi = rne(x), lo = rne(x - hi)), products as hi*hi + hi*lo + lo*hi
+ * with fp32 accumulation.
+ * "split NHWC" activation: uint16 [B][H][W][2C] (per pixel C hi, then C lo).
+ * split weights: uint16 [Cout][2K] (K hi, then K lo), k = (ky*KW + kx)*Cp + ci.
+ * dls_conv_pack_input_f32: NCHW fp32 [B][C][H][W] -> split NHWC with Cp channels
+ * (Cp >= C, a multiple of 32; zeros beyond C).
+ * dls_conv_pack_weights_f32: fp32 [Cout][Cin][KH][KW] -> split weights, Cp as above.
+ * dls_conv_bn_act_split: y = act(bn(conv(x, w)) [+ residual]) in split NHWC;
+ * bn = the exact eval batch norm above (consts = [mean | iv | w | b], or null:
+ * none); residual split NHWC of y's shape or null; relu 0/1.  C a multiple of
+ * 32, Cout of 64; 16-byte aligned pointers; y must not alias x or residual.
+ * dls_pool_linear_split: logits[b][o] = sum_c mean_pixels(x[b])[c] * weight[o][c]
+ * + bias[o] over a split NHWC [B][HW][2C] activation (C <= 2048; bias may be
+ * null), every sum in a fixed order. */
+int dls_conv_pack_input_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, int32_t Cp,
+                            uint16_t *out, dls_stream_t stream);
+int dls_conv_pack_weights_f32(const float *w, int32_t Cout, int32_t Cin, int32_t KH, int32_t KW,
+                              int32_t Cp, uint16_t *out, dls_stream_t stream);
+int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, int32_t C,
+                          const uint16_t *w, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
+                          int32_t pad, const float *consts, const uint16_t *residual, int32_t relu,
+                          uint16_t *y, dls_stream_t stream);
+int dls_pool_linear_split(const uint16_t *x, int64_t B, int32_t HW, int32_t C, const float *weight,
+                          const float *bias, int32_t O, float *out, dls_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
