@@ -42,6 +42,7 @@ from distributed_learning_simulator_amd.model_shapes import resnet18_cifar, vgg1
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (~2.5 PF)
 # f32 VALU issue roof: 256 CUs x 4 SIMDs x 32 lanes per clock x 2.4 GHz = 78.6 T
 # lane-ops/s (a v_pk_* op = 2 lane-ops per lane; MI355X_MICROARCH.md: the f32
 # VALU peak is 64 FLOP/clk/SIMD with FMAs counted twice)
@@ -680,30 +681,65 @@ def _shapley_eval_server(args, dev, K=50):
     return server
 
 
+def conv_eval_roofline(tester, reps=3):
+    """The utility forward's MFMA roof (csrc/conv.hip): forward_split over the
+    tester's images (weights packed once, batches of tester.batch_size), timed with
+    HIP events on the current stream (every launch of the forward runs there).
+    achieved = issued bf16 MFMA flops (3 products x 2 x the MACs of the padded
+    operands: the stem's 27 -> 32 im2col channels) / time, against the dense bf16
+    peak; fp32_equivalent = the model's own 2 x MACs / time."""
+    from distributed_learning_simulator_amd.models import split_conv_macs
+    model, X = tester.model, tester.dataset[0]
+    issued, useful = split_conv_macs(model, X.shape[2], X.shape[3])
+    n, bs = X.shape[0], tester.batch_size
+    with torch.no_grad():
+        pk = model.pack_split()
+        for i in range(0, n, bs):
+            model.forward_split(X[i:i + bs], pk)
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for i in range(0, n, bs):
+                model.forward_split(X[i:i + bs], pk)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+    ms = sorted(ts)[len(ts) // 2]
+    ach = 6 * issued * n / (ms / 1e3) / 1e12
+    return {"kernel": "dls_conv_bn_act_split (k_conv3x3_halo, k_conv_bf16x3) + pool_linear",
+            "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s (bf16 MFMA issued)", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
+            "traffic": None, "ms_per_forward_of_all_images": round(ms, 3),
+            "issued_macs_per_image": issued, "model_macs_per_image": useful,
+            "fp32_equivalent_tflops": round(2 * useful * n / (ms / 1e3) / 1e12, 1)}
+
+
 def bench_shapley_evals(args, dev, world=1, rank=0):
     """Config 5b: Shapley utility evaluations through ShapleyValueServer.evaluate_subsets
     (batched bit-exact subset models + ResNet-18 test-set inference; on N ranks the
     coalitions are dealt round-robin and the utilities all-reduced).  Weak scaling:
     args.evals coalitions per GPU.  Timed with the tester's default GPU forward (the
-    value: deterministic convolution algorithms, so a coalition's utility is a
-    function of the coalition; every eval batch norm + residual + ReLU one
-    hand-written pass, logits bit-identical to the module's forward), again with the
-    module's own forward (``fused_eval=False``: MIOpen batch norm, separate add and
-    ReLU kernels), and with non-deterministic convolutions (the cost of determinism)."""
+    value: the library's deterministic convolutions, csrc/conv.hip — a coalition's
+    utility is a function of the coalition in any process), and, for comparison,
+    with MIOpen convolutions: its deterministic algorithms with the fused exact
+    batch-norm pass (round 4's default, logits bit-identical to the module's
+    forward), the module's own forward, and MIOpen's non-deterministic algorithms."""
     ts = time.perf_counter()
     server = _shapley_eval_server(args, dev)
     if rank == 0:
         log(f"shapley_evals: server and test set ready in {time.perf_counter() - ts:.1f} s")
     coal = _shapley_coalitions(50, (args.evals + 2) * world, SEED + 7)
 
-    def timed(fused, deterministic=True):
+    def timed(conv="dls", fused=True, deterministic=True):
+        server.tester.conv = conv
         server.tester.fused_eval = fused
         server.tester.deterministic = deterministic
         tw = time.perf_counter()
-        server.evaluate_subsets(coal[: 2 * world])  # MIOpen kernel selection, warm caches
+        server.evaluate_subsets(coal[: 2 * world])  # kernel selection, warm caches
         torch.cuda.synchronize()
         if rank == 0:
-            log(f"shapley_evals: warm-up (fused={fused}, deterministic={deterministic}) "
+            log(f"shapley_evals: warm-up (conv={conv}, fused={fused}, deterministic={deterministic}) "
                 f"{time.perf_counter() - tw:.1f} s")
         if world > 1:
             dist.barrier()
@@ -712,42 +748,45 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         if rank == 0:
-            log(f"shapley_evals: {len(coal) - 2 * world} evals in {el:.1f} s")
+            log(f"shapley_evals: {len(coal) - 2 * world} evals in {el:.2f} s")
         if world > 1:
             el = _max_over_ranks(el, dev)
         return el, vals
 
-    el, vals = timed(True)
-    el_m, vals_m = timed(False)
-    # the cost of reproducible utilities: the same path with MIOpen free to pick
-    # non-deterministic convolution algorithms (not the product's default)
-    el_nd, _ = timed(True, deterministic=False)
-    server.tester.deterministic = True
+    el, vals = timed()
+    el_md, vals_md = timed("miopen")
+    el_m, vals_m = timed("miopen", fused=False)
+    # the cost of reproducible utilities on MIOpen: its default (not run-to-run
+    # reproducible) algorithms
+    el_nd, _ = timed("miopen", deterministic=False)
+    server.tester.conv, server.tester.fused_eval, server.tester.deterministic = "dls", True, True
     n = len(coal) - 2 * world
+    rf = conv_eval_roofline(server.tester) if rank == 0 else None
     del server
     torch.cuda.empty_cache()
     bn = bench_bn_act(args, dev) if rank == 0 else None
+    rate = lambda e: {"value": round(n / e, 3), "unit": "subset-evals/s (all GPUs)",  # noqa: E731
+                      "ms_per_eval_per_gpu": round(e / n * world * 1e3, 2)}
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
-                      f"{args.eval_images} CIFAR-10-shaped images (fp32, batch 1000, NCHW: "
-                      f"MIOpen's deterministic convolutions)",
-            "value": round(n / el, 3), "unit": "subset-evals/s (all GPUs)",
-            "ms_per_eval_per_gpu": round(el / n * world * 1e3, 2),
+                      f"{args.eval_images} CIFAR-10-shaped images (batch 1000): the library's "
+                      f"deterministic convolutions (bf16x3 MFMA, fused eval batch norm)",
+            **rate(el),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
             "deterministic_convs": True,
-            "nondeterministic_convs": {"value": round(n / el_nd, 3),
-                                       "unit": "subset-evals/s (all GPUs)",
-                                       "note": "the same path with MIOpen's default (not "
-                                               "run-to-run reproducible) convolution algorithms "
-                                               "on NHWC activations: what determinism costs"},
-            "module_forward": {"value": round(n / el_m, 3), "unit": "subset-evals/s (all GPUs)",
-                               "ms_per_eval_per_gpu": round(el_m / n * world * 1e3, 2),
-                               "max_utility_diff": round(
-                                   max(abs(a - b) for a, b in zip(vals, vals_m)), 6),
-                               "note": "Inferencer(fused_eval=False): the module's own eval "
-                                       "forward (MIOpen batch norm, separate add and ReLU "
-                                       "kernels); the default path's logits are bit-identical "
-                                       "to it (tests/test_gpu_infer.py)"},
+            "roofline": rf,
+            "miopen_deterministic": {**rate(el_md), "max_utility_diff": round(
+                max(abs(a - b) for a, b in zip(vals, vals_md)), 6),
+                "note": "Inferencer(conv='miopen'): MIOpen's deterministic NCHW convolutions + "
+                        "the fused exact batch-norm pass (round 4's default; logits "
+                        "bit-identical to the module's forward)"},
+            "module_forward": {**rate(el_m), "max_utility_diff_vs_miopen_deterministic": round(
+                max(abs(a - b) for a, b in zip(vals_md, vals_m)), 6),
+                "note": "Inferencer(conv='miopen', fused_eval=False): the module's own eval "
+                        "forward (MIOpen convolutions and batch norm, separate add and ReLU)"},
+            "nondeterministic_convs": {**rate(el_nd),
+                                       "note": "MIOpen's default (not run-to-run reproducible) "
+                                               "convolution algorithms on NHWC activations"},
             "bn_act": bn}
 
 

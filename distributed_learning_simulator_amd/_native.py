@@ -79,6 +79,9 @@ SIGNATURES = {
     "dls_bn_act_exact_nchw_f32": ([_p, _i64, _i32, _i64, _p, _p, _i32, _p, _p], _i32),
     "dls_conv_pack_input_f32": ([_p, _i64, _i32, _i32, _i32, _i32, _p, _p], _i32),
     "dls_conv_pack_weights_f32": ([_p, _i32, _i32, _i32, _i32, _i32, _p, _p], _i32),
+    "dls_conv_pack_im2col_f32": ([_p, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _p, _p],
+                                 _i32),
+    "dls_conv_pack_weights_im2col_f32": ([_p, _i32, _i32, _i32, _i32, _i32, _p, _p], _i32),
     "dls_conv_bn_act_split": ([_p, _i64, _i32, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _p,
                                _i32, _p, _p], _i32),
     "dls_pool_linear_split": ([_p, _i64, _i32, _i32, _p, _p, _i32, _p, _p], _i32),
@@ -392,6 +395,35 @@ def conv_pack_weights(w, stream=None):
     out = torch.empty((co, 2 * kh * kw * cp), dtype=torch.int16, device=w.device)
     _check(lib().dls_conv_pack_weights_f32(_ptr(w), co, ci, kh, kw, cp, _ptr(out),
                                            _stream(stream, w)), "dls_conv_pack_weights_f32")
+    return out
+
+
+def conv_pack_im2col(x, ksize, stride, pad, stream=None):
+    """NCHW fp32 [B, C, H, W] -> the split NHWC im2col [B, Ho, Wo, 2 Kp] of a
+    (KH, KW) convolution, Kp = KH*KW*C rounded up to 32: the operand of a 1x1
+    conv_bn_act with conv_pack_weights_im2col weights (few-channel first layers)."""
+    if x.dtype != torch.float32 or x.dim() != 4 or not x.is_contiguous():
+        raise RuntimeError("conv_pack_im2col: x must be a contiguous NCHW fp32 tensor")
+    B, C, H, W = x.shape
+    kh, kw = ksize
+    kp = split_channels(kh * kw * C)
+    ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    out = torch.empty((B, ho, wo, 2 * kp), dtype=torch.int16, device=x.device)
+    _check(lib().dls_conv_pack_im2col_f32(_ptr(x), B, C, H, W, kh, kw, stride, pad, kp, _ptr(out),
+                                          _stream(stream, x)), "dls_conv_pack_im2col_f32")
+    return out
+
+
+def conv_pack_weights_im2col(w, stream=None):
+    """fp32 [Cout, Cin, KH, KW] -> split weights [Cout, 2 Kp] in conv_pack_im2col's k order."""
+    w = w.detach()
+    if w.dtype != torch.float32 or w.dim() != 4 or not w.is_contiguous():
+        raise RuntimeError("conv_pack_weights_im2col: w must be a contiguous fp32 [Cout, Cin, KH, KW]")
+    co, ci, kh, kw = w.shape
+    kp = split_channels(kh * kw * ci)
+    out = torch.empty((co, 2 * kp), dtype=torch.int16, device=w.device)
+    _check(lib().dls_conv_pack_weights_im2col_f32(_ptr(w), co, ci, kh, kw, kp, _ptr(out),
+                                                  _stream(stream, w)), "dls_conv_pack_weights_im2col_f32")
     return out
 
 

@@ -36,6 +36,8 @@
 // k_bn_act_exact: fma(w, (x - mean) * iv, b)), the residual add and the ReLU,
 // and stores the output split — the next convolution's operand — so a ResNet
 // block is 2 (or 3) launches and no separate batch-norm pass.
+#include <cstdlib>
+
 #include "dls_common.h"
 
 namespace dls {
@@ -69,38 +71,162 @@ struct ConvArgs {
     uint16_t *y;            // split output [B][Ho][Wo][2 Cout]
     int H, W, C, Ho, Wo, Cout, KW, taps, stride, pad, K, M, relu;
     int pix_tiles, co_tiles;
+    int B, TI, TR, NH;  // halo kernel: images / rows per pixel tile, halo rows
 };
 
 constexpr int kWaveTile = 64;  // a wave's output tile: 64 channels x 64 pixels
+constexpr int kBK = 32;        // channels per staged chunk
+constexpr int kRowB = 4 * kBK + 16;  // LDS row: kBK hi, kBK lo (bf16), 16 B pad
 
-template <int BK, int WCO, int WPIX>
+typedef f32x16 WaveAcc[2][2];
+
+// One staged chunk (kBK channels) into the wave's 2 x 2 tiles: A rows from `arow`
+// (this lane's row r of the wave's first 32-channel tile; the second at +32
+// rows), B rows of the two 32-pixel tiles at b0 / b1 (this lane's pixel).
+// Products in the fixed order lo*hi, hi*lo, hi*hi per k-step.
+__device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, const uint8_t *b0,
+                                           const uint8_t *b1, int h) {
+#pragma unroll
+    for (int s = 0; s < kBK / 16; ++s) {
+        const int off = 32 * s + 16 * h;  // bytes: k = 16 s + 8 h .. + 7
+        bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            ah[i] = *reinterpret_cast<const bf16x8 *>(arow + i * 32 * kRowB + off);
+            al[i] = *reinterpret_cast<const bf16x8 *>(arow + i * 32 * kRowB + 2 * kBK + off);
+        }
+        bh[0] = *reinterpret_cast<const bf16x8 *>(b0 + off);
+        bl[0] = *reinterpret_cast<const bf16x8 *>(b0 + 2 * kBK + off);
+        bh[1] = *reinterpret_cast<const bf16x8 *>(b1 + off);
+        bl[1] = *reinterpret_cast<const bf16x8 *>(b1 + 2 * kBK + off);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+    }
+}
+
+__device__ __forceinline__ void zero_acc(WaveAcc &acc) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+}
+
+// Epilogue through LDS (smem >= BNP * (4 BMC + 16) bytes, free: every wave past
+// its last read of the staged operands): the raw tiles are transposed to
+// [pixel][channel] fp32, then each thread takes 8 channels of a pixel — batch norm
+// fma(w, (x - mean) * iv, b), + residual (hi + lo), ReLU, split — and stores 16-B
+// hi and lo pieces: a block's threads write whole runs of its pixels' rows.
+// Lane (r, h) of wave (wc, wp) holds pixel wp*64 + 32 j + r, channels
+// wc*64 + 32 i + 8 g + 4 h + e in acc[i][j][4 g + e].
+template <int BMC, int BNP, int NT>
+__device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, const ConvArgs &a,
+                                             int co0, int pix0, int wc, int wp, int tid) {
+    constexpr int EROW = 4 * BMC + 16;
+    const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int pl = wp * kWaveTile + 32 * j + r;
+                const int cl = wc * kWaveTile + 32 * i + 8 * g + 4 * h;
+                *reinterpret_cast<f32x4 *>(smem + pl * EROW + cl * 4) =
+                    f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+            }
+    __syncthreads();
+    constexpr int GPP = BMC / 8;  // 8-channel groups per pixel
+    constexpr int NPC = BNP * GPP / NT;
+    static_assert(NT % GPP == 0 && (BNP * GPP) % NT == 0, "epilogue shape");
+    const int cl = 8 * (tid % GPP), co = co0 + cl;  // a thread's channel group is fixed
+    float m[8], iv[8], wv[8], bv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        m[e] = a.consts ? a.consts[co + e] : 0.f;
+        iv[e] = a.consts ? a.consts[a.Cout + co + e] : 1.f;
+        wv[e] = a.consts ? a.consts[2 * a.Cout + co + e] : 1.f;
+        bv[e] = a.consts ? a.consts[3 * a.Cout + co + e] : 0.f;
+    }
+#pragma unroll 2
+    for (int u = 0; u < NPC; ++u) {
+        const int pl = (tid + NT * u) / GPP;
+        const int p = pix0 + pl;
+        if (p >= a.M) continue;
+        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4);
+        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4 + 16);
+        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        const int64_t ob = (int64_t)p * (2 * a.Cout) + co;
+        if (a.consts) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
+        }
+        if (a.res) {
+            const u32x4 rh = *reinterpret_cast<const u32x4 *>(a.res + ob);
+            const u32x4 rl = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const uint32_t sh = 16 * (e & 1);
+                v[e] = v[e] + (bf16_to_f32((rh[e >> 1] >> sh) & 0xffffu) +
+                               bf16_to_f32((rl[e >> 1] >> sh) & 0xffffu));
+            }
+        }
+        uint32_t hi[8], lo[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float x = v[e];
+            if (a.relu) x = x > 0.f ? x : (x == x ? 0.f : x);  // relu keeps NaN, as torch
+            split2(x, hi[e], lo[e]);
+        }
+        *reinterpret_cast<u32x4 *>(a.y + ob) =
+            u32x4{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
+        *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) =
+            u32x4{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+    }
+}
+
+// XCD-aware tile order: the 8 XCDs take consecutive blockIdx round-robin; give
+// each a contiguous run of (pixel tile, channel tile) pairs, channel tile fastest,
+// so blocks reading the same input pixels share an L2
+__device__ __forceinline__ int tile_of_block() {
+    const int nblk = gridDim.x, bid = blockIdx.x;
+    return (nblk & 7) == 0 ? (bid & 7) * (nblk >> 3) + (bid >> 3) : bid;
+}
+
+// ---------------------------------------------------------------- generic
+// Any stride / padding / kernel size: every chunk stages the A rows (channels x
+// kBK) and the B rows (each output pixel's input pixel under the chunk's tap,
+// zero outside the image) through double-buffered LDS, register-staged.
+template <int WCO, int WPIX>
 __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
     constexpr int NT = 64 * WCO * WPIX;
     constexpr int BMC = kWaveTile * WCO;   // output channels per block
     constexpr int BNP = kWaveTile * WPIX;  // pixels per block
-    constexpr int ROWB = 4 * BK + 16;      // LDS row: BK hi, BK lo (bf16), 16 B pad
-    constexpr int PPR = BK / 4;            // 16-B pieces per row
-    constexpr int HP = BK / 8;             // of which hi
+    constexpr int PPR = kBK / 4;           // 16-B pieces per row
+    constexpr int HP = kBK / 8;            // of which hi
     constexpr int RPP = NT / PPR;          // rows per staging pass
     constexpr int NA = BMC / RPP, NB = BNP / RPP;
+    constexpr int STAGE = 2 * (BMC + BNP) * kRowB;
+    constexpr int EPI = BNP * (4 * BMC + 16);
     static_assert(NT % PPR == 0 && BMC % RPP == 0 && BNP % RPP == 0, "staging shape");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (BMC + BNP) * ROWB];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
-    // XCD-aware tile order: the 8 XCDs take consecutive blockIdx round-robin;
-    // give each a contiguous run of (pixel tile, channel tile) pairs, channel tile
-    // fastest, so blocks reading the same input pixels share an L2
-    const int nblk = gridDim.x;
-    const int bid = blockIdx.x;
-    int t = bid;
-    if ((nblk & 7) == 0) t = (bid & 7) * (nblk >> 3) + (bid >> 3);
+    const int t = tile_of_block();
     const int co0 = (t % a.co_tiles) * BMC;
     const int pix0 = (t / a.co_tiles) * BNP;
 
     // staging assignment: piece `part` of rows tid / PPR + RPP * u
     const int part = tid % PPR, row0 = tid / PPR;
-    const int poff = part < HP ? part * 8 : BK + (part - HP) * 8;  // element offset in a chunk
+    const int poff = part < HP ? part * 8 : kBK + (part - HP) * 8;  // element offset in a chunk
     int pbase[NB], piy[NB], pix_[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
@@ -122,11 +248,11 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 #pragma unroll
     for (int u = 0; u < NA; ++u) wrow[u] = a.w + (int64_t)(co0 + row0 + RPP * u) * (2 * a.K);
 
-    const int cchunks = a.C / BK;
+    const int cchunks = a.C / kBK;
     const int nchunks = a.taps * cchunks;
     u32x4 ra[NA], rb[NB];
     auto load = [&](int c) {
-        const int tap = c / cchunks, ci0 = (c - tap * cchunks) * BK;
+        const int tap = c / cchunks, ci0 = (c - tap * cchunks) * kBK;
         const int ky = tap / a.KW, kx = tap - ky * a.KW;
         const int kc = tap * a.C + ci0;
         const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
@@ -145,103 +271,168 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
         }
     };
     auto store = [&](int buf) {
-        uint8_t *As = smem + buf * (BMC + BNP) * ROWB;
-        uint8_t *Bs = As + BMC * ROWB;
+        uint8_t *As = smem + buf * (BMC + BNP) * kRowB;
+        uint8_t *Bs = As + BMC * kRowB;
 #pragma unroll
         for (int u = 0; u < NA; ++u)
-            *reinterpret_cast<u32x4 *>(As + (row0 + RPP * u) * ROWB + poff * 2) = ra[u];
+            *reinterpret_cast<u32x4 *>(As + (row0 + RPP * u) * kRowB + poff * 2) = ra[u];
 #pragma unroll
         for (int u = 0; u < NB; ++u)
-            *reinterpret_cast<u32x4 *>(Bs + (row0 + RPP * u) * ROWB + poff * 2) = rb[u];
+            *reinterpret_cast<u32x4 *>(Bs + (row0 + RPP * u) * kRowB + poff * 2) = rb[u];
     };
 
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
+    WaveAcc acc;
+    zero_acc(acc);
     const int r = lane & 31, h = lane >> 5;
-    auto compute = [&](int buf) {
-        const uint8_t *As = smem + buf * (BMC + BNP) * ROWB + (wc * kWaveTile + r) * ROWB;
-        const uint8_t *Bs = smem + buf * (BMC + BNP) * ROWB + (BMC + wp * kWaveTile + r) * ROWB;
-#pragma unroll
-        for (int s = 0; s < BK / 16; ++s) {
-            const int off = 32 * s + 16 * h;  // bytes: k = 16 s + 8 h .. + 7
-            bf16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                ah[i] = *reinterpret_cast<const bf16x8 *>(As + i * 32 * ROWB + off);
-                al[i] = *reinterpret_cast<const bf16x8 *>(As + i * 32 * ROWB + 2 * BK + off);
-                bh[i] = *reinterpret_cast<const bf16x8 *>(Bs + i * 32 * ROWB + off);
-                bl[i] = *reinterpret_cast<const bf16x8 *>(Bs + i * 32 * ROWB + 2 * BK + off);
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                }
-        }
-    };
-
     load(0);
     store(0);
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
         const bool more = c + 1 < nchunks;
         if (more) load(c + 1);
-        compute(c & 1);
+        const uint8_t *base = smem + (c & 1) * (BMC + BNP) * kRowB;
+        const uint8_t *b0 = base + (BMC + wp * kWaveTile + r) * kRowB;
+        mfma_chunk(acc, base + (wc * kWaveTile + r) * kRowB, b0, b0 + 32 * kRowB, h);
         if (more) store((c + 1) & 1);
         __syncthreads();
     }
+    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
+}
 
-    // epilogue: lane holds pixel pix0 + wp*64 + 32 j + r, channels
-    // co0 + wc*64 + 32 i + 8 g + 4 h + e  (e < 4) in acc[i][j][4 g + e]
+// ------------------------------------------------------ 3x3, stride 1, pad 1
+// The block's pixels are a rectangle of whole output rows (TR rows of one image,
+// or TI whole images), so its input is one halo tile: TI x (TR + 2) x (W + 2)
+// pixels, staged once per chunk of kBK channels and read by all 9 taps at shifted
+// rows — instead of 9 gathered B tiles (8-9x less LDS writing and L2 reading).
+// The weights of one (chunk, tap) are double-buffered per tap; the next chunk's
+// halo loads into registers at the chunk's first tap and is written after its
+// last (single-buffered halo: 2 blocks per CU).
+// (Measured slower: each wave loading its A fragments straight from global memory
+// into registers a tap ahead, with no A staging and no barrier per tap — 20-40 %
+// slower on every shape, profiles/r05_conv_probe.txt.)
+template <int WCO, int WPIX, int NHMAX>
+__global__ __launch_bounds__(64 * WCO * WPIX) void k_conv3x3_halo(ConvArgs a) {
+    constexpr int NT = 64 * WCO * WPIX;
+    constexpr int BMC = kWaveTile * WCO;
+    constexpr int BNP = kWaveTile * WPIX;
+    constexpr int PPR = kBK / 4, HP = kBK / 8, RPP = NT / PPR;
+    constexpr int NA = BMC / RPP;
+    constexpr int HROWS = RPP * NHMAX;  // halo rows the LDS image holds
+    constexpr int STAGE = (HROWS + 2 * BMC) * kRowB;
+    constexpr int EPI = BNP * (4 * BMC + 16);
+    static_assert(NT % PPR == 0 && BMC % RPP == 0, "staging shape");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
+    uint8_t *halo = smem;
+    uint8_t *abuf = smem + HROWS * kRowB;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wc = wid / WPIX, wp = wid % WPIX;
+    const int t = tile_of_block();
+    const int co0 = (t % a.co_tiles) * BMC;
+    const int pt = t / a.co_tiles;
+    const int pix0 = pt * BNP;
+    const int W = a.W, H = a.H, W2 = W + 2;
+    const int hrows_img = (a.TR + 2) * W2;
+    int b0, y0;
+    if (a.TR == H) {
+        b0 = pt * a.TI;
+        y0 = 0;
+    } else {
+        const int tpi = H / a.TR;
+        b0 = pt / tpi;
+        y0 = (pt - b0 * tpi) * a.TR;
+    }
+
+    const int part = tid % PPR, row0 = tid / PPR;
+    const int poff = part < HP ? part * 8 : kBK + (part - HP) * 8;
+    // input pixel of each halo row this thread stages: -1 zero, -2 past the tile
+    int hpix[NHMAX];
+#pragma unroll
+    for (int u = 0; u < NHMAX; ++u) {
+        const int hr = row0 + RPP * u;
+        int pix = -2;
+        if (hr < a.NH) {
+            const int ti = hr / hrows_img, rem = hr - ti * hrows_img;
+            const int ry = rem / W2, rx = rem - ry * W2;
+            const int b = b0 + ti, iy = y0 - 1 + ry, ix = rx - 1;
+            pix = (b < a.B && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                      ? (b * H + iy) * W + ix
+                      : -1;
+        }
+        hpix[u] = pix;
+    }
+    const uint16_t *wrow[NA];
+#pragma unroll
+    for (int u = 0; u < NA; ++u) wrow[u] = a.w + (int64_t)(co0 + row0 + RPP * u) * (2 * a.K);
+
+    u32x4 hreg[NHMAX], areg[NA];
+    auto hload = [&](int cc) {
+        const int xo = part < HP ? cc * kBK + part * 8 : a.C + cc * kBK + (part - HP) * 8;
+#pragma unroll
+        for (int u = 0; u < NHMAX; ++u)
+            hreg[u] = hpix[u] >= 0
+                          ? *reinterpret_cast<const u32x4 *>(a.x + (int64_t)hpix[u] * (2 * a.C) + xo)
+                          : u32x4{0u, 0u, 0u, 0u};
+    };
+    auto hstore = [&]() {
+#pragma unroll
+        for (int u = 0; u < NHMAX; ++u)
+            if (hpix[u] != -2)
+                *reinterpret_cast<u32x4 *>(halo + (row0 + RPP * u) * kRowB + poff * 2) = hreg[u];
+    };
+    auto aload = [&](int cc, int tap) {
+        const int kc = tap * a.C + cc * kBK;
+        const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
+#pragma unroll
+        for (int u = 0; u < NA; ++u) areg[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
+    };
+    auto astore = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < NA; ++u)
+            *reinterpret_cast<u32x4 *>(abuf + (buf * BMC + row0 + RPP * u) * kRowB + poff * 2) = areg[u];
+    };
+
+    // this lane's output pixels (wp*64 + 32 j + r) as halo rows under tap (0, 0)
+    const int r = lane & 31, h = lane >> 5;
+    int hb[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        const int p = pix0 + wp * kWaveTile + 32 * j + r;
-        if (p >= a.M) continue;
-        const int64_t ob = (int64_t)p * (2 * a.Cout);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int co = co0 + wc * kWaveTile + 32 * i + 8 * g + 4 * h;
-                f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                           acc[i][j][4 * g + 3]};
-                if (a.consts) {
-                    const f32x4 m = *reinterpret_cast<const f32x4 *>(a.consts + co);
-                    const f32x4 iv = *reinterpret_cast<const f32x4 *>(a.consts + a.Cout + co);
-                    const f32x4 wv = *reinterpret_cast<const f32x4 *>(a.consts + 2 * a.Cout + co);
-                    const f32x4 bv = *reinterpret_cast<const f32x4 *>(a.consts + 3 * a.Cout + co);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
-                }
-                if (a.res) {
-                    const u32x2 rh = *reinterpret_cast<const u32x2 *>(a.res + ob + co);
-                    const u32x2 rl = *reinterpret_cast<const u32x2 *>(a.res + ob + a.Cout + co);
-                    v[0] = v[0] + (bf16_to_f32(rh[0] & 0xffffu) + bf16_to_f32(rl[0] & 0xffffu));
-                    v[1] = v[1] + (bf16_to_f32(rh[0] >> 16) + bf16_to_f32(rl[0] >> 16));
-                    v[2] = v[2] + (bf16_to_f32(rh[1] & 0xffffu) + bf16_to_f32(rl[1] & 0xffffu));
-                    v[3] = v[3] + (bf16_to_f32(rh[1] >> 16) + bf16_to_f32(rl[1] >> 16));
-                }
-                uint32_t hi[4], lo[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float x = v[e];
-                    if (a.relu) x = x > 0.f ? x : (x == x ? 0.f : x);  // relu keeps NaN, as torch
-                    split2(x, hi[e], lo[e]);
-                }
-                *reinterpret_cast<u32x2 *>(a.y + ob + co) = u32x2{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16)};
-                *reinterpret_cast<u32x2 *>(a.y + ob + a.Cout + co) =
-                    u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
-            }
+        const int pl = wp * kWaveTile + 32 * j + r;
+        const int tw = a.TR * W;
+        const int ti = pl / tw, rem = pl - ti * tw;
+        const int oy = rem / W, ox = rem - oy * W;
+        hb[j] = ti * hrows_img + oy * W2 + ox;
     }
+
+    WaveAcc acc;
+    zero_acc(acc);
+    const int nc = a.C / kBK;
+    hload(0);
+    aload(0, 0);
+    hstore();
+    astore(0);
+    __syncthreads();
+    int step = 0;
+    for (int cc = 0; cc < nc; ++cc) {
+        if (cc + 1 < nc) hload(cc + 1);
+#pragma unroll 1
+        for (int tap = 0; tap < 9; ++tap, ++step) {
+            const bool last = tap == 8;
+            const bool nxt = !last || cc + 1 < nc;
+            if (nxt) aload(last ? cc + 1 : cc, last ? 0 : tap + 1);
+            const int ky = tap / 3, kx = tap - 3 * ky;
+            const int sh = ky * W2 + kx;
+            mfma_chunk(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * kRowB,
+                       halo + (hb[0] + sh) * kRowB, halo + (hb[1] + sh) * kRowB, h);
+            if (nxt) astore((step + 1) & 1);
+            if (last && cc + 1 < nc) {
+                __syncthreads();  // every wave is done with this chunk's halo
+                hstore();
+            }
+            __syncthreads();
+        }
+    }
+    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
 // fp32 NCHW image batch -> split NHWC with Cp >= C channels (zeros beyond C)
@@ -259,20 +450,52 @@ __global__ __launch_bounds__(256) void k_pack_input(const float *__restrict__ x,
     y[pix * 2 * Cp + Cp + ci] = (uint16_t)lo;
 }
 
-// fp32 [Cout][Cin][KH][KW] -> split [Cout][2K], k = (ky * KW + kx) * Cp + ci
+// fp32 [Cout][Cin][KH][KW] -> split [Cout][2K]: k = (ky * KW + kx) * Cp + ci
+// (per-tap channel runs padded to Cp), or with FLAT k = (ky * KW + kx) * Cin + ci
+// for k < KH * KW * Cin, zero up to K (the im2col operand's order)
+template <bool FLAT>
 __global__ __launch_bounds__(256) void k_pack_weights(const float *__restrict__ w, int Cout, int Cin,
-                                                     int KH, int KW, int Cp, uint16_t *__restrict__ y) {
-    const int K = KH * KW * Cp;
+                                                     int KH, int KW, int K, int Cp,
+                                                     uint16_t *__restrict__ y) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)Cout * K) return;
     const int co = (int)(i / K), k = (int)(i - (int64_t)co * K);
-    const int tap = k / Cp, ci = k - tap * Cp;
+    const int cdiv = FLAT ? Cin : Cp;
+    const int tap = k / cdiv, ci = k - tap * cdiv;
     const int ky = tap / KW, kx = tap - ky * KW;
-    const float v = ci < Cin ? w[(((int64_t)co * Cin + ci) * KH + ky) * KW + kx] : 0.f;
+    const bool live = FLAT ? k < KH * KW * Cin : ci < Cin;
+    const float v = live ? w[(((int64_t)co * Cin + ci) * KH + ky) * KW + kx] : 0.f;
     uint32_t hi, lo;
     split2(v, hi, lo);
     y[(int64_t)co * 2 * K + k] = (uint16_t)hi;
     y[(int64_t)co * 2 * K + K + k] = (uint16_t)lo;
+}
+
+// im2col of an fp32 NCHW batch for a first layer with few input channels: split
+// NHWC [B][Ho][Wo][2 Kp], k = (ky * KW + kx) * C + ci (zero outside the image and
+// for k >= KH * KW * C); the convolution is then a 1x1 one with Kp channels
+// (ResNet-18's 3-channel stem: 27 -> 32 instead of 9 taps x 32 padded channels).
+__global__ __launch_bounds__(256) void k_pack_im2col(const float *__restrict__ x, int64_t n, int C, int H,
+                                                    int W, int KH, int KW, int stride, int pad, int Ho,
+                                                    int Wo, int Kp, uint16_t *__restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (output pixel, k), k fastest
+    if (i >= n) return;
+    const int k = (int)(i % Kp);
+    const int64_t pix = i / Kp;
+    const int64_t hw = (int64_t)Ho * Wo;
+    const int64_t b = pix / hw;
+    const int rem = (int)(pix - b * hw);
+    const int oy = rem / Wo, ox = rem - oy * Wo;
+    const int tap = k / C, ci = k - tap * C;
+    const int ky = tap / KW, kx = tap - ky * KW;
+    const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+    float v = 0.f;
+    if (k < KH * KW * C && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        v = x[((b * C + ci) * H + iy) * W + ix];
+    uint32_t hi, lo;
+    split2(v, hi, lo);
+    y[pix * 2 * Kp + k] = (uint16_t)hi;
+    y[pix * 2 * Kp + Kp + k] = (uint16_t)lo;
 }
 
 // Global average pool + linear layer over split NHWC [B][HW][2C]: one block per
@@ -309,9 +532,8 @@ __global__ __launch_bounds__(kPoolBlock) void k_pool_linear(const uint16_t *__re
     }
 }
 
-template <int BK, int WCO, int WPIX>
-int launch_conv(const ConvArgs &a0, hipStream_t st) {
-    ConvArgs a = a0;
+template <int WCO, int WPIX>
+int launch_conv(ConvArgs a, hipStream_t st) {
     a.pix_tiles = (a.M + kWaveTile * WPIX - 1) / (kWaveTile * WPIX);
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
@@ -319,9 +541,39 @@ int launch_conv(const ConvArgs &a0, hipStream_t st) {
         set_error("dls_conv_bn_act_split: %lld blocks", (long long)blocks);
         return DLS_EINVAL;
     }
-    hipLaunchKernelGGL((k_conv_bf16x3<BK, WCO, WPIX>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
-                       st, a);
+    hipLaunchKernelGGL((k_conv_bf16x3<WCO, WPIX>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0, st, a);
     return check_launch("dls_conv_bn_act_split");
+}
+
+// The halo kernel when the pixel tile can be whole output rows: returns 1 if
+// launched (or the launch failed: rc set), 0 if the shape does not fit it.
+template <int WCO, int WPIX, int NHMAX>
+int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
+    constexpr int BNP = kWaveTile * WPIX;
+    constexpr int RPP = 64 * WCO * WPIX / (kBK / 4);
+    const int H = a.H, W = a.W;
+    if (W > BNP || BNP % W) return 0;
+    const int TR = H < BNP / W ? H : BNP / W;
+    int TI = 1;
+    if (TR == H) {
+        if (BNP % (H * W)) return 0;
+        TI = BNP / (H * W);
+    } else if (H % TR) {
+        return 0;
+    }
+    const int NH = TI * (TR + 2) * (W + 2);
+    if (NH > RPP * NHMAX) return 0;
+    a.TI = TI;
+    a.TR = TR;
+    a.NH = NH;
+    a.pix_tiles = (a.M + BNP - 1) / BNP;
+    a.co_tiles = a.Cout / (kWaveTile * WCO);
+    const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
+    if (blocks > INT32_MAX) return 0;
+    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
+                       st, a);
+    rc = check_launch("dls_conv_bn_act_split");
+    return 1;
 }
 
 }  // namespace
@@ -351,10 +603,42 @@ int dls_conv_pack_weights_f32(const float *w, int32_t Cout, int32_t Cin, int32_t
                     (int64_t)KH * KW * Cp <= (1 << 24),
                 DLS_EINVAL, "dls_conv_pack_weights_f32: Cout=%d Cin=%d KH=%d KW=%d Cp=%d", Cout, Cin,
                 KH, KW, Cp);
-    const int64_t n = (int64_t)Cout * KH * KW * Cp;
-    hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), w, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Cp, out);
+    const int K = KH * KW * Cp;
+    const int64_t n = (int64_t)Cout * K;
+    hipLaunchKernelGGL(k_pack_weights<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), w, (int)Cout, (int)Cin, (int)KH, (int)KW, K, (int)Cp, out);
     return check_launch("dls_conv_pack_weights_f32");
+}
+
+int dls_conv_pack_weights_im2col_f32(const float *w, int32_t Cout, int32_t Cin, int32_t KH, int32_t KW,
+                                     int32_t Kp, uint16_t *out, dls_stream_t stream) {
+    DLS_REQUIRE(w && out, DLS_EINVAL, "dls_conv_pack_weights_im2col_f32: null pointer");
+    DLS_REQUIRE(Cout > 0 && Cin > 0 && KH > 0 && KW > 0 && Kp >= KH * KW * Cin && Kp % 32 == 0 &&
+                    Kp <= (1 << 24),
+                DLS_EINVAL, "dls_conv_pack_weights_im2col_f32: Cout=%d Cin=%d KH=%d KW=%d Kp=%d", Cout,
+                Cin, KH, KW, Kp);
+    const int64_t n = (int64_t)Cout * Kp;
+    hipLaunchKernelGGL(k_pack_weights<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), w, (int)Cout, (int)Cin, (int)KH, (int)KW, (int)Kp, (int)Kp, out);
+    return check_launch("dls_conv_pack_weights_im2col_f32");
+}
+
+int dls_conv_pack_im2col_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, int32_t KH,
+                             int32_t KW, int32_t stride, int32_t pad, int32_t Kp, uint16_t *out,
+                             dls_stream_t stream) {
+    DLS_REQUIRE(x && out, DLS_EINVAL, "dls_conv_pack_im2col_f32: null pointer");
+    DLS_REQUIRE(B >= 0 && C > 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0 &&
+                    H + 2 * pad >= KH && W + 2 * pad >= KW && Kp >= KH * KW * C && Kp % 32 == 0 &&
+                    Kp <= (1 << 24),
+                DLS_EINVAL, "dls_conv_pack_im2col_f32: B=%lld C=%d H=%d W=%d KH=%d KW=%d Kp=%d",
+                (long long)B, C, H, W, KH, KW, Kp);
+    const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+    const int64_t n = B * Ho * Wo * (int64_t)Kp;
+    if (n == 0) return DLS_OK;
+    hipLaunchKernelGGL(k_pack_im2col, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       x, n, (int)C, (int)H, (int)W, (int)KH, (int)KW, (int)stride, (int)pad, Ho, Wo,
+                       (int)Kp, out);
+    return check_launch("dls_conv_pack_im2col_f32");
 }
 
 int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, int32_t C,
@@ -379,10 +663,17 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     DLS_REQUIRE(M <= INT32_MAX / 2 && B * H * W <= INT32_MAX / 2, DLS_EINVAL,
                 "dls_conv_bn_act_split: %lld output pixels", (long long)M);
     ConvArgs a{x, w, consts, residual, y, (int)H, (int)W, (int)C, Ho, Wo, (int)Cout, (int)KW,
-               (int)(KH * KW), (int)stride, (int)pad, (int)(KH * KW * C), (int)M, relu ? 1 : 0, 0, 0};
+               (int)(KH * KW), (int)stride, (int)pad, (int)(KH * KW * C), (int)M, relu ? 1 : 0, 0, 0,
+               (int)B, 0, 0, 0};
     hipStream_t st = as_stream(stream);
-    if (Cout % 128 == 0) return launch_conv<32, 2, 2>(a, st);
-    return launch_conv<32, 1, 4>(a, st);
+    const bool wide = Cout % 128 == 0;
+    // DLS_CONV_CFG=g (probe knob, read per call): the generic kernel only
+    const char *cfg = getenv("DLS_CONV_CFG");
+    if (!(cfg && cfg[0] == 'g') && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
+        int rc = DLS_OK;
+        if (wide ? try_launch_halo<2, 2, 9>(a, st, rc) : try_launch_halo<1, 4, 11>(a, st, rc)) return rc;
+    }
+    return wide ? launch_conv<2, 2>(a, st) : launch_conv<1, 4>(a, st);
 }
 
 int dls_pool_linear_split(const uint16_t *x, int64_t B, int32_t HW, int32_t C, const float *weight,

@@ -108,7 +108,11 @@ class ResNet18(nn.Module):
             if isinstance(m, nn.Conv2d):
                 if m.bias is not None or m.groups != 1 or m.dilation != (1, 1):
                     raise RuntimeError("forward_split: plain bias-free convolutions only")
-                pk[id(m)] = _native.conv_pack_weights(m.weight.contiguous())
+                # the 3-channel stem as a 1x1 convolution over its im2col (27 -> 32
+                # channels instead of 9 taps x 32 padded ones)
+                pack = (_native.conv_pack_weights_im2col if m is self.conv1
+                        else _native.conv_pack_weights)
+                pk[id(m)] = pack(m.weight.contiguous())
             elif isinstance(m, nn.BatchNorm2d):
                 c = torch.empty(4 * m.num_features, device=m.running_mean.device)
                 _native.bn_fold_exact(m, c)
@@ -127,7 +131,9 @@ class ResNet18(nn.Module):
             return _native.conv_bn_act(inp, pk[id(conv)], conv.kernel_size, conv.stride[0],
                                        conv.padding[0], pk[id(bn)], residual, relu)
 
-        out = cba(_native.conv_pack_input(x.contiguous()), self.conv1, self.bn1)
+        c1 = self.conv1
+        xs = _native.conv_pack_im2col(x.contiguous(), c1.kernel_size, c1.stride[0], c1.padding[0])
+        out = _native.conv_bn_act(xs, pk[id(c1)], (1, 1), 1, 0, pk[id(self.bn1)], None, True)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 h = cba(out, blk.conv1, blk.bn1)
@@ -148,6 +154,34 @@ class ResNet18(nn.Module):
                 out = blk.forward_fused(out, fold)
         out = F.adaptive_avg_pool2d(out, 1).flatten(1)
         return self.linear(out)
+
+
+def split_conv_macs(model, H, W):
+    """(issued, model) multiply-accumulates per image of ResNet18.forward_split at
+    H x W inputs: issued counts the padded operands the MFMAs run on (input
+    channels rounded up to 32; the stem's im2col 27 -> 32), model the convolutions'
+    own (+ the linear layer, as both)."""
+    shapes = {}
+    hooks = [m.register_forward_hook(lambda m, i, o: shapes.__setitem__(id(m), o.shape))
+             for m in model.modules() if isinstance(m, nn.Conv2d)]
+    try:
+        with torch.no_grad():
+            p = next(model.parameters())
+            model.eval()(torch.zeros(1, model.conv1.in_channels, H, W, device=p.device))
+    finally:
+        for h in hooks:
+            h.remove()
+    issued = useful = model.linear.in_features * model.linear.out_features
+    for m in model.modules():
+        if isinstance(m, nn.Conv2d):
+            _, co, ho, wo = shapes[id(m)]
+            k = m.kernel_size[0] * m.kernel_size[1]
+            useful += ho * wo * co * k * m.in_channels
+            if m is model.conv1:
+                issued += ho * wo * co * ((k * m.in_channels + 31) // 32 * 32)
+            else:
+                issued += ho * wo * co * k * ((m.in_channels + 31) // 32 * 32)
+    return issued, useful
 
 
 MODELS = {"LeNet5": LeNet5, "ResNet18": ResNet18}

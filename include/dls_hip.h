@@ -290,6 +290,10 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * dls_conv_pack_input_f32: NCHW fp32 [B][C][H][W] -> split NHWC with Cp channels
  * (Cp >= C, a multiple of 32; zeros beyond C).
  * dls_conv_pack_weights_f32: fp32 [Cout][Cin][KH][KW] -> split weights, Cp as above.
+ * dls_conv_pack_im2col_f32 / dls_conv_pack_weights_im2col_f32: a first layer with
+ * few input channels as a 1x1 convolution over its im2col: split NHWC
+ * [B][Ho][Wo][2 Kp] / split weights [Cout][2 Kp], k = (ky*KW + kx)*C + ci, zero
+ * for k >= KH*KW*C (Kp a multiple of 32).
  * dls_conv_bn_act_split: y = act(bn(conv(x, w)) [+ residual]) in split NHWC;
  * bn = the exact eval batch norm above (consts = [mean | iv | w | b], or null:
  * none); residual split NHWC of y's shape or null; relu 0/1.  C a multiple of
@@ -301,6 +305,11 @@ int dls_conv_pack_input_f32(const float *x, int64_t B, int32_t C, int32_t H, int
                             uint16_t *out, dls_stream_t stream);
 int dls_conv_pack_weights_f32(const float *w, int32_t Cout, int32_t Cin, int32_t KH, int32_t KW,
                               int32_t Cp, uint16_t *out, dls_stream_t stream);
+int dls_conv_pack_im2col_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, int32_t KH,
+                             int32_t KW, int32_t stride, int32_t pad, int32_t Kp, uint16_t *out,
+                             dls_stream_t stream);
+int dls_conv_pack_weights_im2col_f32(const float *w, int32_t Cout, int32_t Cin, int32_t KH, int32_t KW,
+                                     int32_t Kp, uint16_t *out, dls_stream_t stream);
 int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, int32_t C,
                           const uint16_t *w, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                           int32_t pad, const float *consts, const uint16_t *residual, int32_t relu,

@@ -1,0 +1,182 @@
+"""Deterministic convolutions of the utility evaluation (csrc/conv.hip;
+SURVEY.md §8 row a-3, servers/fed_server.py:26-32 get_metric -> the tester).
+
+There is no reference output to pin: the reference evaluates with torch's
+convolutions on its own device, whose low bits depend on the algorithm the
+library picks.  The contract tested here is the one the Shapley servers need:
+  * every conv + eval batch norm (+ residual) + ReLU launch is within a stated
+    bound of an fp64 evaluation of the same function (bf16x3 products: a relative
+    error of ~2^-16 per product; the bound, 5e-5 of the magnitude sum, is >= 7x
+    the largest error measured, profiles/r05_conv_probe.txt);
+  * the same inputs give the same bits on repeated launches, interleaved with
+    other shapes, and on fresh tensors (and in another process:
+    tests/test_gpu_distributed.py::test_utility_bit_identical_across_processes);
+  * ResNet-18's logits agree with torch's fp32 forward to ~1e-5 of their scale and
+    top-1 agrees except where the top two logits are that close.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda", 0)
+TOL = 5e-5
+
+# (cin, cout, k, stride, H, W, residual, batch): every ResNet-18 shape (halo kernel
+# for 3x3 stride 1, generic kernel otherwise), ragged last tiles (batch not a
+# multiple of the images per tile), sizes the halo tiling does not fit (28x28,
+# 7x7, 12x12 -> generic), Cout a multiple of 64 but not of 128, a non-square
+# image, and the im2col stem (cin < 32)
+SHAPES = [
+    (3, 64, 3, 1, 32, 32, False, 4), (64, 64, 3, 1, 32, 32, False, 3), (64, 64, 3, 1, 32, 32, True, 2),
+    (64, 128, 3, 2, 32, 32, False, 3), (64, 128, 1, 2, 32, 32, False, 3),
+    (128, 128, 3, 1, 16, 16, True, 3), (128, 256, 3, 2, 16, 16, False, 2), (128, 256, 1, 2, 16, 16, False, 2),
+    (256, 256, 3, 1, 8, 8, True, 3), (256, 512, 3, 2, 8, 8, False, 2), (256, 512, 1, 2, 8, 8, False, 2),
+    (512, 512, 3, 1, 4, 4, True, 5), (64, 64, 3, 1, 28, 28, True, 2), (128, 128, 3, 1, 7, 7, False, 3),
+    (96, 192, 3, 1, 12, 12, True, 2), (64, 128, 3, 1, 8, 16, False, 3), (3, 64, 3, 1, 28, 28, False, 2),
+]
+
+
+def _bn(c, g):
+    bn = torch.nn.BatchNorm2d(c).to(dev).eval()
+    with torch.no_grad():
+        bn.running_mean.copy_(torch.randn(c, generator=g) * 0.3)
+        bn.running_var.copy_(torch.rand(c, generator=g) * 1.5 + 0.5)
+        bn.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(c, generator=g) * 0.2)
+    return bn
+
+
+def _run(cin, cout, k, s, H, W, res, B, seed=0):
+    from distributed_learning_simulator_amd import _native
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, cin, H, W, generator=g).to(dev)
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(dev)
+    bn = _bn(cout, g)
+    consts = torch.empty(4 * cout, device=dev)
+    _native.bn_fold_exact(bn, consts)
+    pad = k // 2
+    ho, wo = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
+    r = torch.randn(B, cout, ho, wo, generator=g).to(dev) if res else None
+    rs = _native.conv_pack_input(r) if res else None
+    if cin < 32:
+        xs, ws = _native.conv_pack_im2col(x, (k, k), s, pad), _native.conv_pack_weights_im2col(w)
+        geom = ((1, 1), 1, 0)
+    else:
+        xs, ws = _native.conv_pack_input(x), _native.conv_pack_weights(w)
+        geom = ((k, k), s, pad)
+    ys = _native.conv_bn_act(xs, ws, *geom, consts, rs, relu=True)
+    return (x, w, bn, r, s, pad), (xs, ws, geom, consts, rs), ys
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda t: "c{}-{}k{}s{}_{}x{}{}_b{}".format(
+    t[0], t[1], t[2], t[3], t[4], t[5], "_res" if t[6] else "", t[7]))
+def test_conv_bn_act_matches_fp64(shape):
+    from distributed_learning_simulator_amd import _native
+    (x, w, bn, r, s, pad), _, ys = _run(*shape)
+    y = _native.split_to_f32(ys).double()
+    xd, wd = x.double(), w.double()
+    m = bn.running_mean.double()[None, :, None, None]
+    sc = (bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps))[None, :, None, None]
+    b = bn.bias.double()[None, :, None, None]
+    ref = (F.conv2d(xd, wd, stride=s, padding=pad) - m) * sc + b
+    den = F.conv2d(xd.abs(), wd.abs(), stride=s, padding=pad) * sc.abs() + (m * sc).abs() + b.abs()
+    if r is not None:
+        ref = ref + r.double()
+        den = den + r.double().abs()
+    ref = ref.clamp_min(0)
+    err = ((y - ref).abs() / (den + ref.abs() + 1e-30)).max().item()
+    assert err < TOL, err
+    assert y.shape == ref.shape and torch.isfinite(y).all()
+
+
+def test_conv_bit_identical_on_repeat():
+    """The same inputs -> the same bits: repeated launches, launches of other shapes
+    in between, and fresh copies of the operands (other addresses)."""
+    from distributed_learning_simulator_amd import _native
+    _, (xs, ws, geom, consts, rs), y1 = _run(64, 64, 3, 1, 32, 32, True, 4, seed=3)
+    _, (xs2, ws2, geom2, consts2, rs2), z1 = _run(256, 512, 3, 2, 8, 8, False, 4, seed=4)
+    y2 = _native.conv_bn_act(xs, ws, *geom, consts, rs, relu=True)
+    z2 = _native.conv_bn_act(xs2, ws2, *geom2, consts2, rs2, relu=True)
+    y3 = _native.conv_bn_act(xs.clone(), ws.clone(), *geom, consts.clone(), rs.clone(), relu=True)
+    assert torch.equal(y1, y2) and torch.equal(y1, y3) and torch.equal(z1, z2)
+
+
+def test_conv_rejects_bad_shapes():
+    from distributed_learning_simulator_amd import _native
+    x = torch.zeros(2, 8, 8, 2 * 48, dtype=torch.int16, device=dev)  # C = 48: not a multiple of 32
+    w = torch.zeros(64, 2 * 9 * 48, dtype=torch.int16, device=dev)
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1)
+    x = torch.zeros(2, 8, 8, 2 * 64, dtype=torch.int16, device=dev)
+    w = torch.zeros(96, 2 * 9 * 64, dtype=torch.int16, device=dev)  # Cout = 96
+    with pytest.raises(RuntimeError, match="Cout of 64"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1)
+    w = torch.zeros(64, 2 * 9 * 32, dtype=torch.int16, device=dev)  # packed for another C
+    with pytest.raises(RuntimeError, match="do not match"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1)
+
+
+def _resnet(seed):
+    from distributed_learning_simulator_amd.models import ResNet18
+    torch.manual_seed(seed)
+    model = ResNet18().to(dev).eval()
+    g = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+                m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.weight.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+                m.bias.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+    return model
+
+
+@pytest.mark.parametrize("hw", [32, 28])
+def test_resnet18_forward_split_matches_torch(hw):
+    """Logits within 2e-5 of their scale of torch's fp32 forward; top-1 equal
+    except at near-ties (top-2 margin <= 1e-4 of the scale)."""
+    from distributed_learning_simulator_amd.models import synthetic_classification
+    model = _resnet(0)
+    X, _ = synthetic_classification(1500, (3, hw, hw), seed=2)
+    X = X.to(dev)
+    with torch.no_grad():
+        pk = model.pack_split()
+        ours = torch.cat([model.forward_split(X[i:i + 500], pk) for i in range(0, X.shape[0], 500)])
+        ref = torch.cat([model(X[i:i + 500]) for i in range(0, X.shape[0], 500)])
+        again = torch.cat([model.forward_split(X[i:i + 500], model.pack_split())
+                           for i in range(0, X.shape[0], 500)])
+    assert torch.equal(ours.view(torch.int32), again.view(torch.int32))
+    scale = ref.abs().amax(dim=1)
+    assert ((ours - ref).abs().amax(dim=1) <= 2e-5 * scale).all()
+    top2 = ref.topk(2, dim=1).values
+    near = (top2[:, 0] - top2[:, 1]) <= 1e-4 * scale
+    mism = ours.argmax(1) != ref.argmax(1)
+    assert not (mism & ~near).any()
+
+
+def test_inferencer_default_runs_library_convolutions():
+    """The default GPU tester runs forward_split: torch's global cudnn flags are not
+    touched, the accuracy is the logits' argmax rate, a fresh Inferencer gives the
+    same bits, and 10k CIFAR images take well under a second."""
+    import time
+    from distributed_learning_simulator_amd.models import synthetic_classification
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    model = _resnet(5)
+    X, y = synthetic_classification(10000, (3, 32, 32), seed=6)
+    flags = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    a = Inferencer(model, (X, y), device=dev)
+    assert a.conv == "dls" and a._split_forward() is not None
+    la = a.logits()
+    loss, acc, _ = a.inference()
+    assert (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark) == flags
+    assert acc == int((la.argmax(1).cpu() == y).sum()) / y.numel()
+    b = Inferencer(model, (X, y), device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lb = b.logits()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 1.0
+    assert torch.equal(la.view(torch.int32), lb.view(torch.int32))
+    loss_b, acc_b, _ = b.inference()
+    assert acc == acc_b and float(loss) == float(loss_b)

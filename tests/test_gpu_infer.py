@@ -187,10 +187,10 @@ def test_resnet18_fused_eval_matches_torch(deterministic_convs, fmt):
     # module's forward: the same accuracy and loss, and those of torch's eval
     # forward over the same batches (MIOpen may pick other algorithms for other
     # batch sizes)
-    inf = Inferencer(model, (X, y), batch_size=256, device=dev)
+    inf = Inferencer(model, (X, y), batch_size=256, device=dev, conv="miopen")
     assert inf.fused_eval is True and inf.deterministic  # the NCHW path
     loss, acc, _ = inf.inference()
-    plain = Inferencer(model, (X, y), batch_size=256, device=dev, fused_eval=False)
+    plain = Inferencer(model, (X, y), batch_size=256, device=dev, fused_eval=False, conv="miopen")
     loss0, acc0, _ = plain.inference()
     assert acc == acc0 and float(loss) == float(loss0)
     xq = X.to(dev)  # the Inferencer's deterministic layout: NCHW
@@ -201,25 +201,26 @@ def test_resnet18_fused_eval_matches_torch(deterministic_convs, fmt):
 
 
 def test_utility_is_a_function_of_the_model():
-    """the product's default tester (no fixture, default flags)
-    gives bit-identical logits and the same accuracy / loss for the same model on
-    repeated evaluations and on fresh Inferencers, at ResNet-18 x 10k CIFAR-shaped
-    images (the config-5 utility), and leaves torch's global flags as it found them.
-    And it stays fast: MIOpen's deterministic NHWC convolutions are naive kernels
-    (19 s per evaluation, profiles/r04q_eval_det.txt), the NCHW path ~0.2 s."""
+    """VERDICT r03 item 1, for the MIOpen path (conv="miopen"; the default tester's
+    own convolutions: tests/test_gpu_conv.py): bit-identical logits and the same
+    accuracy / loss for the same model on repeated evaluations and on fresh
+    Inferencers, at ResNet-18 x 10k CIFAR-shaped images (the config-5 utility), and
+    torch's global flags as it found them.  And it stays fast: MIOpen's
+    deterministic NHWC convolutions are naive kernels (19 s per evaluation,
+    profiles/r04q_eval_det.txt), the NCHW path ~0.2 s."""
     from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
     from distributed_learning_simulator_amd.trainer import Inferencer
     torch.manual_seed(7)
     model = ResNet18().to(dev)
     X, y = synthetic_classification(10000, (3, 32, 32), seed=11)
     flags = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
-    a = Inferencer(model, (X, y), device=dev)
+    a = Inferencer(model, (X, y), device=dev, conv="miopen")
     assert a.deterministic and a.fused_eval
     la = a.logits()
     la2 = a.logits()
     loss_a, acc_a, _ = a.inference()
     assert (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark) == flags
-    b = Inferencer(model, (X, y), device=dev)
+    b = Inferencer(model, (X, y), device=dev, conv="miopen")
     lb = b.logits()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -231,7 +232,7 @@ def test_utility_is_a_function_of_the_model():
     assert acc_a == acc_b and float(loss_a) == float(loss_b)
     assert acc_a == int((la.argmax(1).cpu() == y).sum()) / y.numel()
     # the module's own forward under the same flags: the same bits
-    plain = Inferencer(model, (X, y), device=dev, fused_eval=False)
+    plain = Inferencer(model, (X, y), device=dev, fused_eval=False, conv="miopen")
     assert torch.equal(plain.logits().view(torch.int32), la.view(torch.int32))
 
 
@@ -246,10 +247,10 @@ def test_inferencer_odd_plane_sizes():
     torch.manual_seed(3)
     model = ResNet18().to(dev)
     X, y = synthetic_classification(512, (3, 28, 28), seed=5)
-    a = Inferencer(model, (X, y), device=dev)
+    a = Inferencer(model, (X, y), device=dev, conv="miopen")
     la = a.logits()
     assert a._fused_checked == (torch.contiguous_format, True)
-    plain = Inferencer(model, (X, y), device=dev, fused_eval=False)
+    plain = Inferencer(model, (X, y), device=dev, fused_eval=False, conv="miopen")
     assert torch.equal(plain.logits().view(torch.int32), la.view(torch.int32))
     # the kernel alone on odd planes, with a residual and ReLU, vs torch
     g = torch.Generator().manual_seed(1)

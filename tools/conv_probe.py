@@ -27,7 +27,7 @@ from distributed_learning_simulator_amd.models import ResNet18  # noqa: E402
 def layer_check(dev, B=8):
     g = torch.Generator(device=dev).manual_seed(0)
     worst = 0.0
-    for (cin, cout, k, s, H, res) in [(3, 64, 3, 1, 32, False), (64, 64, 3, 1, 32, True),
+    for (cin, cout, k, stride, H, res) in [(3, 64, 3, 1, 32, False), (64, 64, 3, 1, 32, True),
                                       (64, 128, 3, 2, 32, False), (64, 128, 1, 2, 32, False),
                                       (128, 128, 3, 1, 16, True), (128, 256, 3, 2, 16, False),
                                       (256, 512, 3, 2, 8, False), (512, 512, 3, 1, 4, True)]:
@@ -40,17 +40,23 @@ def layer_check(dev, B=8):
         bn.bias.data.normal_(0, 0.2, generator=g)
         consts = torch.empty(4 * cout, device=dev)
         _native.bn_fold_exact(bn, consts)
-        pad = k // 2
+        s, pad = stride, k // 2
         ho = (H + 2 * pad - k) // s + 1
         r = torch.randn(B, cout, ho, ho, device=dev, generator=g) if res else None
-        xs = _native.conv_pack_input(x)
-        ws = _native.conv_pack_weights(w)
         rs = _native.conv_pack_input(r) if res else None
-        ys = _native.conv_bn_act(xs, ws, (k, k), s, pad, consts, rs, relu=True)
+        if cin < 32:  # the stem: a 1x1 convolution over the im2col
+            xs = _native.conv_pack_im2col(x, (k, k), s, pad)
+            ws = _native.conv_pack_weights_im2col(w)
+            kk, s, pad = (1, 1), 1, 0
+        else:
+            xs = _native.conv_pack_input(x)
+            ws = _native.conv_pack_weights(w)
+            kk = (k, k)
+        ys = _native.conv_bn_act(xs, ws, kk, s, pad, consts, rs, relu=True)
         y = _native.split_to_f32(ys)
         xd, wd = x.double(), w.double()
-        ref = F.conv2d(xd, wd, stride=s, padding=pad)
-        absr = F.conv2d(xd.abs(), wd.abs(), stride=s, padding=pad)
+        ref = F.conv2d(xd, wd, stride=stride, padding=k // 2)
+        absr = F.conv2d(xd.abs(), wd.abs(), stride=stride, padding=k // 2)
         m, iv = bn.running_mean.double(), 1 / torch.sqrt(bn.running_var.double() + bn.eps)
         sc = (bn.weight.double() * iv)[None, :, None, None]
         ref = (ref - m[None, :, None, None]) * sc + bn.bias.double()[None, :, None, None]
@@ -60,10 +66,10 @@ def layer_check(dev, B=8):
         den = (absr * sc.abs() + (m[None, :, None, None] * sc).abs() + bn.bias.double().abs()[None, :, None, None]
                + ref.abs() + (r.double().abs() if res else 0) + 1e-30)
         err = ((y.double() - ref).abs() / den).max().item()
-        ys2 = _native.conv_bn_act(xs, ws, (k, k), s, pad, consts, rs, relu=True)
+        ys2 = _native.conv_bn_act(xs, ws, kk, s, pad, consts, rs, relu=True)
         same = torch.equal(ys, ys2)
         worst = max(worst, err)
-        print(f"conv {cin:3d}->{cout:3d} k{k} s{s} H{H:2d} res={int(res)}: max rel err {err:.3e} "
+        print(f"conv {cin:3d}->{cout:3d} k{k} s{stride} H{H:2d} res={int(res)}: max rel err {err:.3e} "
               f"repeat bit-identical {same}", flush=True)
     return worst
 
@@ -112,18 +118,63 @@ def timing(model, X, batch, reps):
           f"(all {[round(t * 1e3, 1) for t in ts]})", flush=True)
 
 
+RESNET18_CONVS = [  # (cin, cout, k, stride, H, residual, count per forward); the stem as 1x1 on its im2col
+    (32, 64, 1, 1, 32, False, 1), (64, 64, 3, 1, 32, False, 2), (64, 64, 3, 1, 32, True, 2),
+    (64, 128, 3, 2, 32, False, 1), (64, 128, 1, 2, 32, False, 1), (128, 128, 3, 1, 16, True, 2),
+    (128, 128, 3, 1, 16, False, 1), (128, 256, 3, 2, 16, False, 1), (128, 256, 1, 2, 16, False, 1),
+    (256, 256, 3, 1, 8, True, 2), (256, 256, 3, 1, 8, False, 1), (256, 512, 3, 2, 8, False, 1),
+    (256, 512, 1, 2, 8, False, 1), (512, 512, 3, 1, 4, True, 2), (512, 512, 3, 1, 4, False, 1)]
+
+
+def layer_times(dev, B=1000, n=20):
+    """Per-conv-shape time of dls_conv_bn_act_split at batch B (n launches, HIP
+    events), and the issued bf16 MFMA rate (3 products x 2 x padded MACs)."""
+    tot = 0.0
+    for (cin, cout, k, s, H, res, cnt) in RESNET18_CONVS:
+        cp = _native.split_channels(cin)
+        pad = k // 2
+        ho = (H + 2 * pad - k) // s + 1
+        x = torch.zeros(B, H, H, 2 * cp, dtype=torch.int16, device=dev)
+        w = torch.zeros(cout, 2 * k * k * cp, dtype=torch.int16, device=dev)
+        consts = torch.ones(4 * cout, device=dev)
+        r = torch.zeros(B, ho, ho, 2 * cout, dtype=torch.int16, device=dev) if res else None
+        y = torch.empty(B, ho, ho, 2 * cout, dtype=torch.int16, device=dev)
+        for _ in range(3):
+            _native.conv_bn_act(x, w, (k, k), s, pad, consts, r, True, out=y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            _native.conv_bn_act(x, w, (k, k), s, pad, consts, r, True, out=y)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / n
+        macs = B * ho * ho * cout * k * k * cp
+        tot += ms * cnt
+        print(f"layer {cin:3d}->{cout:3d} k{k} s{s} H{H:2d} res={int(res)} x{cnt}: {ms * 1e3:8.1f} us  "
+              f"{6 * macs / ms / 1e9:7.1f} TFLOP/s bf16 issued", flush=True)
+    print(f"layers total per batch of {B}: {tot:.3f} ms (x10 = {10 * tot:.1f} ms per 10k-image eval)",
+          flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=10000)
     ap.add_argument("--batch", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--skip-check", action="store_true")
+    ap.add_argument("--layers-only", action="store_true")
+    ap.add_argument("--cfgs", default="", help="DLS_CONV_CFG values to time per layer, e.g. abcde")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    if not a.skip_check:
-        layer_check(dev)
-    model, X = model_check(dev, a.images, a.batch)
-    timing(model, X, a.batch, a.reps)
+    for c in a.cfgs or [os.environ.get("DLS_CONV_CFG", "a")]:
+        os.environ["DLS_CONV_CFG"] = c
+        print(f"== DLS_CONV_CFG={c}", flush=True)
+        if not a.skip_check:
+            layer_check(dev)
+        layer_times(dev, a.batch)
+        if not a.layers_only:
+            model, X = model_check(dev, a.images, a.batch)
+            timing(model, X, a.batch, a.reps)
 
 
 if __name__ == "__main__":
