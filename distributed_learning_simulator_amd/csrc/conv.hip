@@ -26,16 +26,24 @@
 //   weights      uint16 [Cout][2K], per output channel K hi then K lo,
 //                k = (ky * KW + kx) * C + ci (C = the input's padded channels).
 // Implicit GEMM, D[co][pixel] = sum_k W[co][k] X[k][pixel]: A = weights (rows =
-// output channels), B = the input pixels' channel runs, gathered per tap (zero
-// outside the image); so a lane's 16-element MFMA fragment is one 16-B piece of
-// a pixel's hi (or lo) channel run.  Each block stages A and B chunks of BK
-// channels of one tap through double-buffered LDS (register staging, rows padded
-// by 16 B: conflict-free ds_read_b128 fragments), each wave owns a 64 x 64
-// (channel x pixel) output tile = 2 x 2 MFMA tiles.  The epilogue applies the
-// eval batch norm with the batch-norm library's arithmetic (infer.hip,
-// k_bn_act_exact: fma(w, (x - mean) * iv, b)), the residual add and the ReLU,
-// and stores the output split — the next convolution's operand — so a ResNet
-// block is 2 (or 3) launches and no separate batch-norm pass.
+// output channels), B = the input pixels' channel runs under a tap (zero outside
+// the image), so a lane's 16-element MFMA fragment is one 16-B piece of a
+// pixel's hi (or lo) channel run.  Each wave owns a 64 x 64 (channel x pixel)
+// output tile = 2 x 2 MFMA tiles; operands are staged in chunks of 32 channels
+// through LDS (register staging, rows padded by 16 B: conflict-free
+// ds_read_b128 fragments).  Two kernels:
+//   k_conv3x3_halo  3x3 stride-1 convolutions: the block's pixels are whole
+//                   output rows, so its input is ONE halo tile staged once per
+//                   channel chunk and read by all 9 taps at shifted rows;
+//   k_conv_bf16x3   anything else (stride 2, 1x1, sizes the halo tiling does
+//                   not fit): every (tap, chunk) gathers its B tile.
+// The epilogue goes through LDS: the raw tile is transposed to [pixel][channel]
+// and each thread applies the eval batch norm with the batch-norm library's
+// arithmetic (infer.hip, k_bn_act_exact: fma(w, (x - mean) * iv, b)), the
+// residual add and the ReLU to 8 channels of a pixel and stores 16-B hi and lo
+// pieces — the next convolution's operand — so a ResNet block is 2 (or 3)
+// launches and no separate batch-norm pass.  Measured per layer and variant:
+// profiles/r05_conv_probe.txt, DESIGN.md §4.
 #include <cstdlib>
 
 #include "dls_common.h"

@@ -56,7 +56,7 @@ typedef void *dls_stream_t;
 const char *dls_last_error(void);
 int dls_abi_version(void);
 /* First 16 hex digits of the SHA-256 of the library's sources and headers
- * (the csrc .hip sources, csrc/dls_common.h, include/dls_hip.h, concatenated in build
+ * (the csrc .hip sources, csrc/dls_common.h, csrc/quant_common.h, include/dls_hip.h, concatenated in build
  * order), fixed at build time: ties a loaded library to its source tree. */
 const char *dls_source_hash(void);
 int dls_device_count(void);
