@@ -84,6 +84,8 @@ SIGNATURES = {
     "dls_conv_pack_weights_im2col_f32": ([_p, _i32, _i32, _i32, _i32, _i32, _p, _p], _i32),
     "dls_conv_bn_act_split": ([_p, _i64, _i32, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p, _p,
                                _i32, _p, _p], _i32),
+    "dls_conv_stem_bn_act_f32": ([_p, _i64, _i32, _i32, _i32, _p, _i32, _i32, _i32, _i32, _i32, _p,
+                                  _i32, _p, _p], _i32),
     "dls_pool_linear_split": ([_p, _i64, _i32, _i32, _p, _p, _i32, _p, _p], _i32),
 }
 
@@ -447,6 +449,25 @@ def conv_bn_act(x, w, ksize, stride, pad, consts=None, residual=None, relu=True,
     _check(lib().dls_conv_bn_act_split(_ptr(x), B, H, W, c2 // 2, _ptr(w), cout, kh, kw, stride,
                                        pad, _ptr(consts), _ptr(residual), int(bool(relu)),
                                        _ptr(out), _stream(stream, x)), "dls_conv_bn_act_split")
+    return out
+
+
+def conv_stem_bn_act(x, w, ksize, stride, pad, consts=None, relu=True, stream=None):
+    """A few-channel first layer straight from the NCHW fp32 batch x (the im2col
+    fused; KH*KW*C <= 32): y = act(bn(conv(x))) split NHWC
+    (dls_conv_stem_bn_act_f32); w from conv_pack_weights_im2col."""
+    if x.dtype != torch.float32 or x.dim() != 4 or not x.is_contiguous():
+        raise RuntimeError("conv_stem_bn_act: x must be a contiguous NCHW fp32 tensor")
+    B, C, H, W = x.shape
+    kh, kw = ksize
+    cout = w.shape[0]
+    if w.dtype != torch.int16 or w.shape[1] != 2 * 32 or not w.is_contiguous():
+        raise RuntimeError("conv_stem_bn_act: w must be conv_pack_weights_im2col output with Kp = 32")
+    ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
+    out = torch.empty((B, ho, wo, 2 * cout), dtype=torch.int16, device=x.device)
+    _check(lib().dls_conv_stem_bn_act_f32(_ptr(x), B, C, H, W, _ptr(w), cout, kh, kw, stride, pad,
+                                          _ptr(consts), int(bool(relu)), _ptr(out),
+                                          _stream(stream, x)), "dls_conv_stem_bn_act_f32")
     return out
 
 

@@ -318,20 +318,27 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // (Measured slower: each wave loading its A fragments straight from global memory
 // into registers a tap ahead, with no A staging and no barrier per tap — 20-40 %
 // slower on every shape, profiles/r05_conv_probe.txt.)
-template <int WCO, int WPIX, int NHMAX>
-__global__ __launch_bounds__(64 * WCO * WPIX) void k_conv3x3_halo(ConvArgs a) {
+// SKEW: halo row hr at hr * kRowB + (hr / 16) * 16 bytes, so that rows 16 apart
+// (which the 32-pixel MFMA tiles of 4- to 16-wide images read in one pass) fall
+// in different banks: 1-3 % faster on those layers, 3 % slower on 32-wide ones
+// (profiles/r05_conv_probe.txt), so the launcher skews for W <= 16.  Loading the
+// weights two (chunk, tap) steps ahead instead of one changed nothing (same file).
+template <int WCO, int WPIX, int NHMAX, bool SKEW = false>
+__global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a) {
     constexpr int NT = 64 * WCO * WPIX;
     constexpr int BMC = kWaveTile * WCO;
     constexpr int BNP = kWaveTile * WPIX;
     constexpr int PPR = kBK / 4, HP = kBK / 8, RPP = NT / PPR;
     constexpr int NA = BMC / RPP;
     constexpr int HROWS = RPP * NHMAX;  // halo rows the LDS image holds
-    constexpr int STAGE = (HROWS + 2 * BMC) * kRowB;
+    constexpr int HBYTES = HROWS * kRowB + (SKEW ? (HROWS / 16 + 1) * 16 : 0);
+    constexpr int STAGE = HBYTES + 2 * BMC * kRowB;
     constexpr int EPI = BNP * (4 * BMC + 16);
     static_assert(NT % PPR == 0 && BMC % RPP == 0, "staging shape");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *halo = smem;
-    uint8_t *abuf = smem + HROWS * kRowB;
+    uint8_t *abuf = smem + HBYTES;
+    auto hoff = [](int hr) { return hr * kRowB + (SKEW ? (hr >> 4) * 16 : 0); };
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
@@ -386,7 +393,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv3x3_halo(ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < NHMAX; ++u)
             if (hpix[u] != -2)
-                *reinterpret_cast<u32x4 *>(halo + (row0 + RPP * u) * kRowB + poff * 2) = hreg[u];
+                *reinterpret_cast<u32x4 *>(halo + hoff(row0 + RPP * u) + poff * 2) = hreg[u];
     };
     auto aload = [&](int cc, int tap) {
         const int kc = tap * a.C + cc * kBK;
@@ -430,8 +437,8 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv3x3_halo(ConvArgs a) {
             if (nxt) aload(last ? cc + 1 : cc, last ? 0 : tap + 1);
             const int ky = tap / 3, kx = tap - 3 * ky;
             const int sh = ky * W2 + kx;
-            mfma_chunk(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * kRowB,
-                       halo + (hb[0] + sh) * kRowB, halo + (hb[1] + sh) * kRowB, h);
+            mfma_chunk(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * kRowB, halo + hoff(hb[0] + sh),
+                       halo + hoff(hb[1] + sh), h);
             if (nxt) astore((step + 1) & 1);
             if (last && cc + 1 < nc) {
                 __syncthreads();  // every wave is done with this chunk's halo
@@ -441,6 +448,83 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv3x3_halo(ConvArgs a) {
         }
     }
     epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
+}
+
+// ------------------------------------------------------------------ stem
+// A first layer whose whole reduction is one chunk (KH * KW * C <= kBK: the
+// 3-channel 3x3 stem of a CIFAR ResNet, 27 terms): the im2col is fused — each
+// thread gathers its output pixel's inputs straight from the fp32 NCHW image
+// batch (k = (ky * KW + kx) * C + ci, zero outside the image and past the 27),
+// splits them and writes the pixel's B row to LDS — then one chunk of MFMAs and
+// the LDS epilogue.  Weights: dls_conv_pack_weights_im2col_f32 with Kp = kBK.
+// CIN / KHW > 0: the input channels and the (square) kernel size as constants
+// (the index arithmetic of the 27-term gather folds away); 0: runtime a.C / a.KW.
+template <int WPIX, int CIN = 0, int KHW = 0>
+__global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float *__restrict__ x) {
+    constexpr int NT = 64 * WPIX, BMC = kWaveTile, BNP = kWaveTile * WPIX;
+    constexpr int PPR = kBK / 4, HP = kBK / 8, RPP = NT / PPR, NA = BMC / RPP;
+    constexpr int STAGE = (BMC + BNP) * kRowB;
+    constexpr int EPI = BNP * (4 * BMC + 16);
+    static_assert(NT == BNP, "one pixel row per thread");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
+    uint8_t *As = smem, *Bs = smem + BMC * kRowB;
+    const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
+    const int t = tile_of_block();
+    const int co0 = (t % a.co_tiles) * BMC;
+    const int pix0 = (t / a.co_tiles) * BNP;
+    // weights: piece `part` of rows tid / PPR + RPP * u
+    const int part = tid % PPR, row0 = tid / PPR;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+        const int row = row0 + RPP * u;
+        const int wo = part < HP ? part * 8 : a.K + (part - HP) * 8;
+        *reinterpret_cast<u32x4 *>(As + row * kRowB + part * 16) =
+            *reinterpret_cast<const u32x4 *>(a.w + (int64_t)(co0 + row) * (2 * a.K) + wo);
+    }
+    // this thread's pixel: gather, split, one LDS row
+    {
+        const int p = pix0 + tid;
+        uint32_t hw[kBK / 2], lw[kBK / 2];
+#pragma unroll
+        for (int q = 0; q < kBK / 2; ++q) hw[q] = lw[q] = 0u;
+        if (p < a.M) {
+            const int hwo = a.Ho * a.Wo;
+            const int b = p / hwo, rem = p - b * hwo;
+            const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
+            const int C = CIN > 0 ? CIN : a.C, KW = KHW > 0 ? KHW : a.KW;
+            const int nk = CIN > 0 ? CIN * KHW * KHW : a.taps * a.C;
+#pragma unroll
+            for (int k = 0; k < kBK; ++k) {
+                float v = 0.f;
+                if (k < nk) {
+                    const int tap = k / C, ci = k - tap * C;
+                    const int ky = tap / KW, kx = tap - ky * KW;
+                    const int iy = oy * a.stride - a.pad + ky, ix = ox * a.stride - a.pad + kx;
+                    if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                        v = x[(((int64_t)b * C + ci) * a.H + iy) * a.W + ix];
+                }
+                uint32_t hi, lo;
+                split2(v, hi, lo);
+                hw[k >> 1] |= hi << (16 * (k & 1));
+                lw[k >> 1] |= lo << (16 * (k & 1));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kBK / 8; ++q) {
+            *reinterpret_cast<u32x4 *>(Bs + tid * kRowB + 16 * q) =
+                u32x4{hw[4 * q], hw[4 * q + 1], hw[4 * q + 2], hw[4 * q + 3]};
+            *reinterpret_cast<u32x4 *>(Bs + tid * kRowB + 2 * kBK + 16 * q) =
+                u32x4{lw[4 * q], lw[4 * q + 1], lw[4 * q + 2], lw[4 * q + 3]};
+        }
+    }
+    __syncthreads();
+    WaveAcc acc;
+    zero_acc(acc);
+    const int r = lane & 31, h = lane >> 5;
+    const uint8_t *b0 = Bs + (wp * kWaveTile + r) * kRowB;
+    mfma_chunk(acc, As + r * kRowB, b0, b0 + 32 * kRowB, h);
+    __syncthreads();  // the epilogue reuses the operands' LDS
+    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, 0, wp, tid);
 }
 
 // fp32 NCHW image batch -> split NHWC with Cp >= C channels (zeros beyond C)
@@ -555,7 +639,7 @@ int launch_conv(ConvArgs a, hipStream_t st) {
 
 // The halo kernel when the pixel tile can be whole output rows: returns 1 if
 // launched (or the launch failed: rc set), 0 if the shape does not fit it.
-template <int WCO, int WPIX, int NHMAX>
+template <int WCO, int WPIX, int NHMAX, bool SKEW>
 int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
     constexpr int RPP = 64 * WCO * WPIX / (kBK / 4);
@@ -578,7 +662,7 @@ int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     if (blocks > INT32_MAX) return 0;
-    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
+    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX, SKEW>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
                        st, a);
     rc = check_launch("dls_conv_bn_act_split");
     return 1;
@@ -679,9 +763,47 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     const char *cfg = getenv("DLS_CONV_CFG");
     if (!(cfg && cfg[0] == 'g') && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
-        if (wide ? try_launch_halo<2, 2, 9>(a, st, rc) : try_launch_halo<1, 4, 11>(a, st, rc)) return rc;
+        const bool skew = W <= 16;
+        const int hit = wide ? (skew ? try_launch_halo<2, 2, 9, true>(a, st, rc)
+                                     : try_launch_halo<2, 2, 9, false>(a, st, rc))
+                             : (skew ? try_launch_halo<1, 4, 11, true>(a, st, rc)
+                                     : try_launch_halo<1, 4, 11, false>(a, st, rc));
+        if (hit) return rc;
     }
     return wide ? launch_conv<2, 2>(a, st) : launch_conv<1, 4>(a, st);
+}
+
+int dls_conv_stem_bn_act_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, const uint16_t *w,
+                             int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
+                             const float *consts, int32_t relu, uint16_t *y, dls_stream_t stream) {
+    DLS_REQUIRE(x && w && y, DLS_EINVAL, "dls_conv_stem_bn_act_f32: null pointer");
+    DLS_REQUIRE(B >= 0 && C > 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && KH * KW * C <= kBK &&
+                    Cout >= 64 && Cout % 64 == 0 && stride > 0 && pad >= 0 && H + 2 * pad >= KH &&
+                    W + 2 * pad >= KW,
+                DLS_EINVAL,
+                "dls_conv_stem_bn_act_f32: B=%lld C=%d H=%d W=%d Cout=%d KH=%d KW=%d (KH*KW*C <= %d, "
+                "Cout a multiple of 64)",
+                (long long)B, C, H, W, Cout, KH, KW, kBK);
+    DLS_REQUIRE(aligned16(w) && aligned16(y) && (!consts || aligned16(consts)), DLS_ELAYOUT,
+                "dls_conv_stem_bn_act_f32: 16-byte alignment");
+    const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+    const int64_t M = B * Ho * Wo;
+    if (M == 0) return DLS_OK;
+    DLS_REQUIRE(M <= INT32_MAX / 2, DLS_EINVAL, "dls_conv_stem_bn_act_f32: %lld output pixels",
+                (long long)M);
+    constexpr int WPIX = 4;
+    ConvArgs a{nullptr, w, consts, nullptr, y, (int)H, (int)W, (int)C, Ho, Wo, (int)Cout, (int)KW,
+               (int)(KH * KW), (int)stride, (int)pad, kBK, (int)M, relu ? 1 : 0, 0, 0, (int)B, 0, 0, 0};
+    a.pix_tiles = (int)((M + kWaveTile * WPIX - 1) / (kWaveTile * WPIX));
+    a.co_tiles = Cout / kWaveTile;
+    const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
+    DLS_REQUIRE(blocks <= INT32_MAX, DLS_EINVAL, "dls_conv_stem_bn_act_f32: %lld blocks", (long long)blocks);
+    if (C == 3 && KH == 3 && KW == 3)  // the CIFAR ResNet stem
+        hipLaunchKernelGGL((k_conv_stem<WPIX, 3, 3>), dim3((unsigned)blocks), dim3(64 * WPIX), 0,
+                           as_stream(stream), a, x);
+    else
+        hipLaunchKernelGGL(k_conv_stem<WPIX>, dim3((unsigned)blocks), dim3(64 * WPIX), 0, as_stream(stream), a, x);
+    return check_launch("dls_conv_stem_bn_act_f32");
 }
 
 int dls_pool_linear_split(const uint16_t *x, int64_t B, int32_t HW, int32_t C, const float *weight,

@@ -132,8 +132,12 @@ class ResNet18(nn.Module):
                                        conv.padding[0], pk[id(bn)], residual, relu)
 
         c1 = self.conv1
-        xs = _native.conv_pack_im2col(x.contiguous(), c1.kernel_size, c1.stride[0], c1.padding[0])
-        out = _native.conv_bn_act(xs, pk[id(c1)], (1, 1), 1, 0, pk[id(self.bn1)], None, True)
+        if c1.kernel_size[0] * c1.kernel_size[1] * c1.in_channels <= 32:  # the im2col fused
+            out = _native.conv_stem_bn_act(x.contiguous(), pk[id(c1)], c1.kernel_size, c1.stride[0],
+                                           c1.padding[0], pk[id(self.bn1)], True)
+        else:
+            xs = _native.conv_pack_im2col(x.contiguous(), c1.kernel_size, c1.stride[0], c1.padding[0])
+            out = _native.conv_bn_act(xs, pk[id(c1)], (1, 1), 1, 0, pk[id(self.bn1)], None, True)
         for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in layer:
                 h = cba(out, blk.conv1, blk.bn1)

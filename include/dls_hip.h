@@ -298,6 +298,9 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * bn = the exact eval batch norm above (consts = [mean | iv | w | b], or null:
  * none); residual split NHWC of y's shape or null; relu 0/1.  C a multiple of
  * 32, Cout of 64; 16-byte aligned pointers; y must not alias x or residual.
+ * dls_conv_stem_bn_act_f32: the same for a first layer whose reduction is one chunk
+ * (KH*KW*C <= 32: a 3-channel 3x3 stem), straight from the fp32 NCHW image batch
+ * (the im2col fused), w from dls_conv_pack_weights_im2col_f32 (Kp = 32).
  * dls_pool_linear_split: logits[b][o] = sum_c mean_pixels(x[b])[c] * weight[o][c]
  * + bias[o] over a split NHWC [B][HW][2C] activation (C <= 2048; bias may be
  * null), every sum in a fixed order. */
@@ -314,6 +317,9 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
                           const uint16_t *w, int32_t Cout, int32_t KH, int32_t KW, int32_t stride,
                           int32_t pad, const float *consts, const uint16_t *residual, int32_t relu,
                           uint16_t *y, dls_stream_t stream);
+int dls_conv_stem_bn_act_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, const uint16_t *w,
+                             int32_t Cout, int32_t KH, int32_t KW, int32_t stride, int32_t pad,
+                             const float *consts, int32_t relu, uint16_t *y, dls_stream_t stream);
 int dls_pool_linear_split(const uint16_t *x, int64_t B, int32_t HW, int32_t C, const float *weight,
                           const float *bias, int32_t O, float *out, dls_stream_t stream);
 

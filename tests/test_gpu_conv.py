@@ -26,7 +26,8 @@ TOL = 5e-5
 # for 3x3 stride 1, generic kernel otherwise), ragged last tiles (batch not a
 # multiple of the images per tile), sizes the halo tiling does not fit (28x28,
 # 7x7, 12x12 -> generic), Cout a multiple of 64 but not of 128, a non-square
-# image, and the im2col stem (cin < 32)
+# image, and the stem (cin < 32: im2col + the generic kernel, and the fused-im2col
+# stem kernel, which must give the same bits)
 SHAPES = [
     (3, 64, 3, 1, 32, 32, False, 4), (64, 64, 3, 1, 32, 32, False, 3), (64, 64, 3, 1, 32, 32, True, 2),
     (64, 128, 3, 2, 32, 32, False, 3), (64, 128, 1, 2, 32, 32, False, 3),
@@ -66,6 +67,9 @@ def _run(cin, cout, k, s, H, W, res, B, seed=0):
         xs, ws = _native.conv_pack_input(x), _native.conv_pack_weights(w)
         geom = ((k, k), s, pad)
     ys = _native.conv_bn_act(xs, ws, *geom, consts, rs, relu=True)
+    if cin < 32 and not res:  # the fused-im2col stem kernel: the same operands, the same bits
+        stem = _native.conv_stem_bn_act(x, ws, (k, k), s, pad, consts, relu=True)
+        assert torch.equal(stem, ys)
     return (x, w, bn, r, s, pad), (xs, ws, geom, consts, rs), ys
 
 

@@ -52,7 +52,7 @@ def main(specs):
             src = os.path.join(tree, "pkg", "csrc")
             os.makedirs(src, exist_ok=True)
             os.makedirs(os.path.join(tree, "include"), exist_ok=True)
-            for f in SRCS + ["dls_common.h"]:
+            for f in SRCS + ["dls_common.h", "quant_common.h"]:
                 try:
                     blob = subprocess.check_output(
                         ["git", "-C", ROOT, "show",

@@ -152,8 +152,22 @@ def layer_times(dev, B=1000, n=20):
         tot += ms * cnt
         print(f"layer {cin:3d}->{cout:3d} k{k} s{s} H{H:2d} res={int(res)} x{cnt}: {ms * 1e3:8.1f} us  "
               f"{6 * macs / ms / 1e9:7.1f} TFLOP/s bf16 issued", flush=True)
-    print(f"layers total per batch of {B}: {tot:.3f} ms (x10 = {10 * tot:.1f} ms per 10k-image eval)",
-          flush=True)
+    # the fused-im2col stem (forward_split's first layer), replacing the 1x1 row above
+    x = torch.randn(B, 3, 32, 32, device=dev)
+    w = _native.conv_pack_weights_im2col(torch.randn(64, 3, 3, 3, device=dev))
+    consts = torch.ones(4 * 64, device=dev)
+    for _ in range(3):
+        _native.conv_stem_bn_act(x, w, (3, 3), 1, 1, consts)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        _native.conv_stem_bn_act(x, w, (3, 3), 1, 1, consts)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    print(f"stem (fused im2col) 3-> 64 k3 s1 H32: {ms * 1e3:8.1f} us", flush=True)
+    print(f"layers total per batch of {B}: {tot:.3f} ms (x10 = {10 * tot:.1f} ms per 10k-image eval; "
+          f"the stem row as the 1x1 conv over its im2col)", flush=True)
 
 
 def main():
