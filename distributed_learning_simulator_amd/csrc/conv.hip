@@ -321,8 +321,11 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // SKEW: halo row hr at hr * kRowB + (hr / 16) * 16 bytes, so that rows 16 apart
 // (which the 32-pixel MFMA tiles of 4- to 16-wide images read in one pass) fall
 // in different banks: 1-3 % faster on those layers, 3 % slower on 32-wide ones
-// (profiles/r05_conv_probe.txt), so the launcher skews for W <= 16.  Loading the
-// weights two (chunk, tap) steps ahead instead of one changed nothing (same file).
+// (profiles/r05_conv_probe.txt), so the launcher skews for W <= 16.  Measured and
+// dropped (same file): the weights loaded two (chunk, tap) steps ahead instead of
+// one (no change); the weights of a whole kernel row (3 taps) staged at once, two
+// barriers per 3 taps instead of one per tap (layer1 -3 %, the 128-512-channel
+// layers +30-45 %: one block per CU).
 template <int WCO, int WPIX, int NHMAX, bool SKEW = false>
 __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a) {
     constexpr int NT = 64 * WCO * WPIX;
