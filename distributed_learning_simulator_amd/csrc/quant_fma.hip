@@ -74,6 +74,14 @@ constexpr int kFmaWps = DLS_FMA_WPS;  // waves per SIMD per launch piece
 #ifndef DLS_FMA_SIDE_PRIO
 #define DLS_FMA_SIDE_PRIO 0  // issue priority of the fp32 / small-int side waves (3: +1 %)
 #endif
+// A piece with fewer than 80 % of its waves on 3-4 KiB tiles (ResNet-18's last:
+// 766 of 994, the rest 1x1-conv tiles of <= 1 KiB that finish early) leaves SIMDs
+// without a stream; its waves keep DS x the clients in flight: 1000 x ResNet-18
+// 1.717-1.727 -> 1.665-1.668 ms (DS 3: 1.728-1.734), VGG-16 unchanged, the same
+// bits (profiles/r05_quant_fma_ab.txt, r05p2).
+#ifndef DLS_FMA_SPARSE_DS
+#define DLS_FMA_SPARSE_DS 2
+#endif
 #ifndef DLS_FMA_F32U
 #define DLS_FMA_F32U 16  // clients per batch of the fp32 side walk (two batches in flight)
 #endif
@@ -190,15 +198,17 @@ __device__ __forceinline__ dls_qtile uniform_tile(const dls_qtile *p) {
 #ifndef DLS_FMA_DN
 #define DLS_FMA_DN 1
 #endif
-template <int G>
+// DS: x DS clients in flight, for a piece whose wide tiles leave SIMDs without a
+// stream (DLS_FMA_SPARSE_DS, the launcher's choice per piece)
+template <int G, int DS = 1>
 constexpr int ring_depth() {
-    return (DLS_FMA_DN == 0 || G >= 3) ? kFmaD : (G == 2 ? 2 * kFmaD : 4 * kFmaD);
+    return DS * ((DLS_FMA_DN == 0 || G >= 3) ? kFmaD : (G == 2 ? 2 * kFmaD : 4 * kFmaD));
 }
 
-template <int G, bool SIGNED>
+template <int G, bool SIGNED, int DS = 1>
 __device__ __forceinline__ void fma_tile(const dls_qtile &t, const FmaCall &a, int rf0, float wf0,
                                          int rf1, float wf1, float *buf) {
-    constexpr int D = ring_depth<G>();
+    constexpr int D = ring_depth<G, DS>();
     f32x2(*tab)[64] = reinterpret_cast<f32x2(*)[64]>(buf);  // [kFmaSpan + 1][64]
     const int lane = __lane_id();
     const int K = a.K;
@@ -339,6 +349,7 @@ struct FmaSide {
 
 // One launch piece: wave w of the piece walks tiles qbase + w + i * nwaves < qend
 // (T tiles per wave, the launcher sizes the piece so).
+template <int DS>
 __global__ __launch_bounds__(kFmaBlock) void k_dequant_fma_stream(const dls_qtile *__restrict__ tiles,
                                                                   FmaPlan plan, FmaCall a, int qbase,
                                                                   int qend, FmaSide side) {
@@ -372,13 +383,13 @@ __global__ __launch_bounds__(kFmaBlock) void k_dequant_fma_stream(const dls_qtil
         auto by_width = [&](auto sgn) {
             constexpr bool SG = decltype(sgn)::value;
             if (kFmaGMax >= 4 && slices >= 4)
-                fma_tile<(kFmaGMax >= 4 ? 4 : 1), SG>(t, a, rf0, wf0, rf1, wf1, buf);
+                fma_tile<(kFmaGMax >= 4 ? 4 : 1), SG, DS>(t, a, rf0, wf0, rf1, wf1, buf);
             else if (kFmaGMax >= 3 && slices == 3)
-                fma_tile<(kFmaGMax >= 3 ? 3 : 1), SG>(t, a, rf0, wf0, rf1, wf1, buf);
+                fma_tile<(kFmaGMax >= 3 ? 3 : 1), SG, DS>(t, a, rf0, wf0, rf1, wf1, buf);
             else if (kFmaGMax >= 2 && slices == 2)
-                fma_tile<(kFmaGMax >= 2 ? 2 : 1), SG>(t, a, rf0, wf0, rf1, wf1, buf);
+                fma_tile<(kFmaGMax >= 2 ? 2 : 1), SG, DS>(t, a, rf0, wf0, rf1, wf1, buf);
             else
-                fma_tile<1, SG>(t, a, rf0, wf0, rf1, wf1, buf);
+                fma_tile<1, SG, DS>(t, a, rf0, wf0, rf1, wf1, buf);
         };
         if (t.kind == 1)
             by_width(std::true_type{});
@@ -420,7 +431,7 @@ int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, cons
     // the kernel's registers allow resident; pieces of equal size (a part-filled
     // last piece would stream at part rate)
     const int64_t resident = std::min<int64_t>(
-        (int64_t)resident_blocks(reinterpret_cast<const void *>(k_dequant_fma_stream), kFmaBlock, 0) *
+        (int64_t)resident_blocks(reinterpret_cast<const void *>(k_dequant_fma_stream<1>), kFmaBlock, 0) *
             wpb,
         (int64_t)device_cus() * 4 * kFmaWps);
     const int T = kFmaT > 0 ? kFmaT : (K <= 256 ? 2 : 1);
@@ -435,8 +446,19 @@ int launch_dequant_fma_stream(const dls_qtile *tiles, const int32_t *nfast, cons
         const int64_t waves = std::min<int64_t>(resident, (m + T - 1) / T);  // T tiles per wave
         side.main_blocks = (int)((waves + wpb - 1) / wpb);
         const int extra = q0 == 0 ? side_blocks : 0;
-        hipLaunchKernelGGL(k_dequant_fma_stream, dim3((unsigned)(side.main_blocks + extra)),
-                           dim3(kFmaBlock), 0, st, tiles, plan, a, (int)q0, (int)q0 + m, side);
+        // tiles of 3-4 KiB slices in this piece (the plan runs widest first)
+        int64_t wide = 0;
+        for (int s = 0; s < 8; ++s)
+            if (4 - order[s] % 4 >= 3)
+                wide += std::max<int64_t>(0, std::min<int64_t>(q0 + m, plan.cum[s + 1]) -
+                                                 std::max<int64_t>(q0, plan.cum[s]));
+        const bool sparse = DLS_FMA_SPARSE_DS > 1 && T == 1 && wide * 5 < waves * 4;
+        if (sparse)
+            hipLaunchKernelGGL(k_dequant_fma_stream<DLS_FMA_SPARSE_DS>, dim3((unsigned)(side.main_blocks + extra)),
+                               dim3(kFmaBlock), 0, st, tiles, plan, a, (int)q0, (int)q0 + m, side);
+        else
+            hipLaunchKernelGGL(k_dequant_fma_stream<1>, dim3((unsigned)(side.main_blocks + extra)),
+                               dim3(kFmaBlock), 0, st, tiles, plan, a, (int)q0, (int)q0 + m, side);
     }
     return check_launch("dls_dequant_fedavg_mode (fma)");
 }
