@@ -35,6 +35,9 @@ SHAPES = [
     (256, 256, 3, 1, 8, 8, True, 3), (256, 512, 3, 2, 8, 8, False, 2), (256, 512, 1, 2, 8, 8, False, 2),
     (512, 512, 3, 1, 4, 4, True, 5), (64, 64, 3, 1, 28, 28, True, 2), (128, 128, 3, 1, 7, 7, False, 3),
     (96, 192, 3, 1, 12, 12, True, 2), (64, 128, 3, 1, 8, 16, False, 3), (3, 64, 3, 1, 28, 28, False, 2),
+    # stems off the 3x3 / 3-channel fast path: a 5x5 MNIST-like one (runtime
+    # index arithmetic) and a strided one over two 64-channel output tiles
+    (1, 64, 5, 1, 28, 28, False, 2), (3, 128, 3, 2, 32, 32, False, 2),
 ]
 
 

@@ -70,6 +70,52 @@ def test_dequant_rejects_bad_mode_without_gpu(lib):
     assert rc == -1 and b"nfast[7]" in lib.dls_last_error()
 
 
+def test_conv_rejects_bad_shapes_without_gpu():
+    """The convolution entry points validate shapes and alignment before any
+    device call (the pointers below are never dereferenced)."""
+    from distributed_learning_simulator_amd import _native
+    L = _native.lib()
+    d = ctypes.c_void_p(256)  # 16-byte aligned, never dereferenced
+    # C = 48: not a multiple of 32
+    rc = L.dls_conv_bn_act_split(d, 2, 8, 8, 48, d, 64, 3, 3, 1, 1, None, None, 1, d, None)
+    assert rc == -1 and b"multiple of 32" in L.dls_last_error()
+    # Cout = 96: not a multiple of 64
+    rc = L.dls_conv_bn_act_split(d, 2, 8, 8, 64, d, 96, 3, 3, 1, 1, None, None, 1, d, None)
+    assert rc == -1 and b"Cout" in L.dls_last_error()
+    # misaligned output
+    rc = L.dls_conv_bn_act_split(d, 2, 8, 8, 64, d, 64, 3, 3, 1, 1, None, None, 1,
+                                 ctypes.c_void_p(258), None)
+    assert rc == -2 and b"alignment" in L.dls_last_error()
+    # a stem whose reduction exceeds one 32-deep chunk (4 channels x 3 x 3 = 36)
+    rc = L.dls_conv_stem_bn_act_f32(d, 2, 4, 8, 8, d, 64, 3, 3, 1, 1, None, 1, d, None)
+    assert rc == -1 and b"KH*KW*C" in L.dls_last_error()
+    rc = L.dls_conv_pack_im2col_f32(d, 2, 3, 8, 8, 3, 3, 1, 1, 16, d, None)  # Kp < 27
+    assert rc == -1
+    rc = L.dls_pool_linear_split(d, 2, 16, 4096, d, None, 10, d, None)  # C > 2048
+    assert rc == -1 and b"C <= 2048" in L.dls_last_error()
+    assert _native.split_channels(3) == 32 and _native.split_channels(64) == 64
+
+
+def test_split_conv_macs_counts_resnet18():
+    """The MAC counts the bench's conv roofline uses: ResNet-18 at 32x32 has
+    555,422,720 multiply-accumulates per image (the textbook 0.56 GMAC), and the
+    library issues the stem's 27 -> 32 padding on top."""
+    from distributed_learning_simulator_amd.models import ResNet18, split_conv_macs
+    issued, useful = split_conv_macs(ResNet18(), 32, 32)
+    assert useful == 555_422_720
+    assert issued - useful == 32 * 32 * 64 * (32 - 27)
+
+
+def test_inferencer_rejects_unknown_conv():
+    import pytest
+    import torch
+    from distributed_learning_simulator_amd.models import LeNet5
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    with pytest.raises(ValueError, match="conv"):
+        Inferencer(LeNet5(), (torch.zeros(1, 1, 32, 32), torch.zeros(1, dtype=torch.long)),
+                   device=torch.device("cpu"), conv="cudnn")
+
+
 def test_product_path_has_no_oracle_import():
     """The shipped package must not import the CPU oracle (no CPU fallback)."""
     pkg = os.path.join(ROOT, "distributed_learning_simulator_amd")
