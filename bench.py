@@ -691,7 +691,7 @@ def conv_eval_roofline(tester, reps=3):
     from distributed_learning_simulator_amd.models import split_conv_macs
     model, X = tester.model, tester.dataset[0]
     issued, useful = split_conv_macs(model, X.shape[2], X.shape[3])
-    n, bs = X.shape[0], tester.batch_size
+    n, bs = X.shape[0], max(tester.batch_size, tester.SPLIT_MIN_BATCH)  # the Inferencer's own
     with torch.no_grad():
         pk = model.pack_split()
         for i in range(0, n, bs):
@@ -769,8 +769,9 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
                       "ms_per_eval_per_gpu": round(e / n * world * 1e3, 2)}
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
-                      f"{args.eval_images} CIFAR-10-shaped images (batch 1000): the library's "
-                      f"deterministic convolutions (bf16x3 MFMA, fused eval batch norm)",
+                      f"{args.eval_images} CIFAR-10-shaped images (tester batch 1000, forward "
+                      f"batches of 2048): the library's deterministic convolutions (bf16x3 MFMA, "
+                      f"fused eval batch norm)",
             **rate(el),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
             "deterministic_convs": True,

@@ -105,6 +105,8 @@ class Inferencer:
     differ it runs the module's forward).  ``fused_eval=False`` always runs the
     module's forward."""
 
+    SPLIT_MIN_BATCH = 2048  # images per forward_split call (at least)
+
     def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True,
                  deterministic=True, conv="dls"):
         if conv not in ("dls", "miopen"):
@@ -182,10 +184,15 @@ class Inferencer:
         self.model.eval()
         split = self._split_forward()
         if split is not None:
+            # the library's convolutions give every image the same bits whatever
+            # batch it runs in (tests/test_gpu_conv.py), so the forward takes at
+            # least SPLIT_MIN_BATCH images at a time: 2000-image batches run a
+            # 10k-image evaluation 4 % faster than 1000 (profiles/r05_conv_probe.txt)
+            bs = max(self.batch_size, self.SPLIT_MIN_BATCH)
             pk = self.model.pack_split()
-            for i in range(0, X.shape[0], self.batch_size):
-                xb = X[i:i + self.batch_size].to(self.device, torch.float32, non_blocking=True)
-                yb = y[i:i + self.batch_size].to(self.device, non_blocking=True)
+            for i in range(0, X.shape[0], bs):
+                xb = X[i:i + bs].to(self.device, torch.float32, non_blocking=True)
+                yb = y[i:i + bs].to(self.device, non_blocking=True)
                 yield split(xb.contiguous(), pk), yb
             return
         fmt = self._memory_format()

@@ -162,6 +162,21 @@ def test_resnet18_forward_split_matches_torch(hw):
     assert not (mism & ~near).any()
 
 
+def test_logits_do_not_depend_on_the_batching():
+    """Each image's logits are the same bits in any batch (the kernels' reduction
+    order per output does not depend on the other images), which lets the
+    Inferencer pick its own forward batch."""
+    from distributed_learning_simulator_amd.models import synthetic_classification
+    model = _resnet(9)
+    X, _ = synthetic_classification(1200, (3, 32, 32), seed=4)
+    X = X.to(dev)
+    with torch.no_grad():
+        pk = model.pack_split()
+        whole = model.forward_split(X, pk)
+        parts = torch.cat([model.forward_split(X[i:i + 173], pk) for i in range(0, X.shape[0], 173)])
+    assert torch.equal(whole.view(torch.int32), parts.view(torch.int32))
+
+
 def test_inferencer_default_runs_library_convolutions():
     """The default GPU tester runs forward_split: torch's global cudnn flags are not
     touched, the accuracy is the logits' argmax rate, a fresh Inferencer gives the

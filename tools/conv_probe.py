@@ -178,6 +178,7 @@ def main():
     ap.add_argument("--skip-check", action="store_true")
     ap.add_argument("--layers-only", action="store_true")
     ap.add_argument("--cfgs", default="", help="DLS_CONV_CFG values to time per layer, e.g. abcde")
+    ap.add_argument("--batches", default="", help="extra forward batch sizes to time, e.g. 2000,5000")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     for c in a.cfgs or [os.environ.get("DLS_CONV_CFG", "a")]:
@@ -189,6 +190,15 @@ def main():
         if not a.layers_only:
             model, X = model_check(dev, a.images, a.batch)
             timing(model, X, a.batch, a.reps)
+            for b in [int(x) for x in a.batches.split(",") if x]:
+                timing(model, X, b, a.reps)
+            if a.batches:  # the logits do not depend on the batching
+                with torch.no_grad():
+                    pk = model.pack_split()
+                    l1 = torch.cat([model.forward_split(X[i:i + a.batch], pk) for i in range(0, X.shape[0], a.batch)])
+                    b = int(a.batches.split(",")[-1])
+                    l2 = torch.cat([model.forward_split(X[i:i + b], pk) for i in range(0, X.shape[0], b)])
+                print(f"logits batch {a.batch} vs {b} bit-identical: {torch.equal(l1, l2)}", flush=True)
 
 
 if __name__ == "__main__":
