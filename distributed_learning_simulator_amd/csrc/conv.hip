@@ -325,7 +325,8 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // dropped (same file): the weights loaded two (chunk, tap) steps ahead instead of
 // one (no change); the weights of a whole kernel row (3 taps) staged at once, two
 // barriers per 3 taps instead of one per tap (layer1 -3 %, the 128-512-channel
-// layers +30-45 %: one block per CU).
+// layers +30-45 %: one block per CU); 8-wave blocks, one per CU (512 pixels x 64
+// channels: layer1 +15-18 %; 256 x 128: +2-10 %).
 template <int WCO, int WPIX, int NHMAX, bool SKEW = false>
 __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a) {
     constexpr int NT = 64 * WCO * WPIX;
