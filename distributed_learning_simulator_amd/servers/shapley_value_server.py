@@ -15,6 +15,7 @@ from itertools import chain, combinations
 import torch
 import torch.distributed as dist
 
+from ..model_util import ModelUtil
 from .fed_server import FedServer
 
 
@@ -45,6 +46,11 @@ class ShapleyValueServer(FedServer):
         values = [0.0] * len(subsets)
         store = self.parameters.store
         bs = self._batch_size()
+        # the default accuracy metric on a tester that can count without a host
+        # synchronisation: the batch's evaluations are queued back to back and
+        # their counts read once (int(count) / n: the same floats as get_metric)
+        queued = (type(self).get_metric is FedServer.get_metric and self.tester is not None
+                  and hasattr(self.tester, "correct_async"))
         for b0 in range(0, len(mine), bs):
             idx = mine[b0:b0 + bs]
             nonempty = [i for i in idx if subsets[i]]
@@ -53,10 +59,20 @@ class ShapleyValueServer(FedServer):
                 rows = [[self.parameters.row_of(w) for w in subsets[i]] for i in nonempty]
                 out = store.subset_models(rows, self.parameters.n_of_row(), method=self.subset_method)
             pos = {i: k for k, i in enumerate(nonempty)}
+            pending = []
             for i in idx:
                 model = store.layout.views(out[pos[i]]) if subsets[i] else self.prev_model
-                values[i] = float(self.get_metric(model))
+                if queued:
+                    ModelUtil(self.tester.model).load_parameter_dict(model)
+                    pending.append((i, self.tester.correct_async()))
+                else:
+                    values[i] = float(self.get_metric(model))
                 self.evaluated_subsets.append(subsets[i])
+            if pending:
+                n = self.tester.dataset[0].shape[0]
+                counts = torch.stack([c for _, c in pending]).tolist()  # one synchronisation
+                for (i, _), c in zip(pending, counts):
+                    values[i] = int(c) / n
         if world > 1:
             t = torch.tensor(values, dtype=torch.float64, device=self.device)
             dist.all_reduce(t)

@@ -219,6 +219,18 @@ class Inferencer:
             return torch.cat([out for out, _ in self._batches()])
 
     @torch.no_grad()
+    def correct_async(self):
+        """The top-1 correct count over the dataset as a device int64 tensor, with
+        no host synchronisation: ``inference()``'s accuracy is ``int(count) / n``.
+        The Shapley servers queue a batch of coalitions' evaluations this way and
+        read all counts with one synchronisation."""
+        with self._flags():
+            correct = torch.zeros((), dtype=torch.int64, device=self.device)
+            for out, yb in self._batches():
+                correct += (out.argmax(1) == yb).sum()
+        return correct
+
+    @torch.no_grad()
     def inference(self):
         with self._flags():
             correct = torch.zeros((), dtype=torch.int64, device=self.device)
