@@ -326,7 +326,12 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // one (no change); the weights of a whole kernel row (3 taps) staged at once, two
 // barriers per 3 taps instead of one per tap (layer1 -3 %, the 128-512-channel
 // layers +30-45 %: one block per CU); 8-wave blocks, one per CU (512 pixels x 64
-// channels: layer1 +15-18 %; 256 x 128: +2-10 %).
+// channels: layer1 +15-18 %; 256 x 128: +2-10 %); persistent blocks that load the
+// next tile's first halo chunk during this tile's epilogue (layer1 +0-2 %, 512
+// channels -3 %, 10-22 VGPRs spilled: a wash).  What does bound it (the same file,
+// r05x2): with one bf16 product per k-step instead of three the layers take
+// 65-85 % of their time — the staging, the fragments' LDS reads and the barriers
+// barely overlap the MFMAs at two waves per SIMD.
 template <int WCO, int WPIX, int NHMAX, bool SKEW = false>
 __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a) {
     constexpr int NT = 64 * WCO * WPIX;
