@@ -49,8 +49,9 @@ class ShapleyValueServer(FedServer):
         # the default accuracy metric on a tester that can count without a host
         # synchronisation: the batch's evaluations are queued back to back and
         # their counts read once (int(count) / n: the same floats as get_metric)
-        queued = (type(self).get_metric is FedServer.get_metric and self.tester is not None
-                  and hasattr(self.tester, "correct_async"))
+        # (not when a subclass or the instance replaces get_metric)
+        queued = (getattr(self.get_metric, "__func__", None) is FedServer.get_metric
+                  and self.tester is not None and hasattr(self.tester, "correct_async"))
         for b0 in range(0, len(mine), bs):
             idx = mine[b0:b0 + bs]
             nonempty = [i for i in idx if subsets[i]]

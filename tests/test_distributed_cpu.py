@@ -360,3 +360,58 @@ def test_sharded_fed_quant_chunked_pipeline(world):
                          [(nm, shape) for nm, shape, _ in shapes])
     got = out[0][1]
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-6
+
+
+def test_queued_evaluations_match_get_metric(monkeypatch):
+    """ShapleyValueServer.evaluate_subsets queues the default accuracy metric on a
+    tester with correct_async (one host synchronisation per batch) and gives the
+    floats get_metric gives; a get_metric replaced on the instance is honoured."""
+    import torch
+    from distributed_learning_simulator_amd.servers.fed_server import FedServer
+    from distributed_learning_simulator_amd.servers.shapley_value_server import ShapleyValueServer
+
+    class _Tester:
+        def __init__(self):
+            self.model = torch.nn.Linear(2, 1)
+            self.dataset = (torch.zeros(7, 2), torch.zeros(7, dtype=torch.long))
+            self.calls = []
+
+        def count(self):
+            return int(round(float(self.model.weight.detach().sum()))) % 8
+
+        def correct_async(self):
+            self.calls.append("async")
+            return torch.tensor(self.count())
+
+        def inference(self):
+            self.calls.append("sync")
+            self.accuracy_metric.value = self.count() / 7
+
+    class _Acc:
+        value = None
+
+        def get_accuracy(self, _epoch=1):
+            return self.value
+
+    class _Params(dict):
+        store = None
+
+    from tests import cpu_doubles
+    cpu_doubles.install(monkeypatch)
+    tester = _Tester()
+    tester.accuracy_metric = _Acc()
+    server = ShapleyValueServer(tester=tester, worker_number=3, synchronous=True,
+                                device=torch.device("cpu"))
+    models = [{"weight": torch.full((1, 2), float(k)), "bias": torch.zeros(1)} for k in range(3)]
+    server._set_prev_model(models[0])
+    # no coalition members: every utility is the previous model's (no store needed)
+    server.parameters = _Params()
+    server._batch_size = lambda: 2
+    got = server.evaluate_subsets([(), (), ()])
+    assert tester.calls == ["async"] * 3
+    want = []
+    for _ in range(3):
+        want.append(FedServer.get_metric(server, server.prev_model))
+    assert got == want
+    server.get_metric = lambda model, metric_type="acc": 0.5  # replaced on the instance
+    assert server.evaluate_subsets([()]) == [0.5]
