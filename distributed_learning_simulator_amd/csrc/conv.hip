@@ -328,7 +328,11 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // layers +30-45 %: one block per CU); 8-wave blocks, one per CU (512 pixels x 64
 // channels: layer1 +15-18 %; 256 x 128: +2-10 %); persistent blocks that load the
 // next tile's first halo chunk during this tile's epilogue (layer1 +0-2 %, 512
-// channels -3 %, 10-22 VGPRs spilled: a wash).  What does bound it (the same file,
+// channels -3 %, 10-22 VGPRs spilled: a wash); a ring of three weight buffers on
+// the 64-channel layers (78 KB, still two blocks per CU) so that each wave reads
+// the next tap's first k-step fragments before the barrier and resumes its MFMAs
+// right after it (layer1 -0.1 to -0.6 %: the barrier's restart latency is not what
+// bounds it).  What does bound it (the same file,
 // r05x2): with one bf16 product per k-step instead of three the layers take
 // 65-85 % of their time — the staging, the fragments' LDS reads and the barriers
 // barely overlap the MFMAs at two waves per SIMD.
