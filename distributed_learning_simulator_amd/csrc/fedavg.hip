@@ -255,6 +255,12 @@ struct UnionDiv {
 // and stores them after staging the next tile, so its next loads never wait
 // behind its stores.  Per membership: one ds_read_b128 of t (4 parameters), the
 // quotient (2 ops two-constant / 3 Markstein, element pairs packed) and the add.
+// (With 50 coalitions the plan leaves two waves 4 coalitions and the rest 3: the
+// most loaded wave carries ~1.18 x the mean.  Measured and dropped: PAIRS of
+// tiles per barrier interval, 2S units (coalition, tile) dealt by the same LPT
+// (~1.08 x the mean), staging between two barriers — bit-identical and 1.4 %
+// slower, 1.818 vs 1.793 ms, profiles/r05_union_pairs.txt: the barrier's wait
+// for the most loaded wave is not what bounds this kernel.)
 //
 // f32x4 add as 2 v_pk_add_f32 (packed fp32 issues two lanes' elements at the
 // cost of one scalar op: tools/valu_rate_probe.hip measured 75 vs 38 T lane-op/s)
