@@ -259,8 +259,11 @@ struct UnionDiv {
 // most loaded wave carries ~1.18 x the mean.  Measured and dropped: PAIRS of
 // tiles per barrier interval, 2S units (coalition, tile) dealt by the same LPT
 // (~1.08 x the mean), staging between two barriers — bit-identical and 1.4 %
-// slower, 1.818 vs 1.793 ms, profiles/r05_union_pairs.txt: the barrier's wait
-// for the most loaded wave is not what bounds this kernel.)
+// slower, 1.818 vs 1.793 ms, profiles/r05_union_ab.txt: the barrier's wait
+// for the most loaded wave is not what bounds this kernel.  Its waves are parked
+// on s_waitcnt / the barrier 60 % of their cycles and issue VALU 14 % (x 4 waves
+// per SIMD: the SIMD's VALU ~56 % busy), same file; reading each group's member
+// offsets two groups ahead of its t reads took 1.5 % off.)
 //
 // f32x4 add as 2 v_pk_add_f32 (packed fp32 issues two lanes' elements at the
 // cost of one scalar op: tools/valu_rate_probe.hip measured 75 vs 38 T lane-op/s)
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
     __shared__ f32x4 ts[2][kUnionChunk * 64];                   // 2 x 64 KiB
     // member byte offsets in a t buffer (client j: j * 1 KiB), per coalition; a
     // wave reads 4 at a time as one broadcast ds_read_b128 (no readlane per member)
-    __shared__ __attribute__((aligned(16))) uint32_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk + 4];
+    __shared__ __attribute__((aligned(16))) uint32_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk + 8];  // + the offsets read ahead
     __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];                 // UnionDiv, per coalition
     __shared__ int lens[DLS_SUBSET_UNION_MAX];
     __shared__ int plan[W][kUnionKMax + 1];                        // [0] = count, then coalitions
@@ -404,11 +407,6 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             auto tload = [&](int l) {
                 return *reinterpret_cast<const f32x4 *>(tb + ml[l]);
             };
-            auto tload4 = [&](int l, f32x4 (&x)[4]) {  // members l..l+3 (l % 4 == 0)
-                const u32x4 o = *reinterpret_cast<const u32x4 *>(ml + l);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f32x4 *>(tb + o[u]);
-            };
             if (__builtin_expect(tile_fast, 1)) {
                 // the coalition's constants as SGPRs (pk ops take them with op_sel,
                 // no VGPR pair copies)
@@ -444,21 +442,32 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
                                     q3 = quot(x[3]);
                         acc = addu(addu(addu(addu(acc, q0), q1), q2), q3);
                     };
-                    auto fetch4 = [&](int l0, f32x4 (&x)[4]) { tload4(l0, x); };
+                    // a group's 4 member offsets are read two groups ahead of its t
+                    // (the t reads depend on them: read just before, their latency
+                    // would stall the wave once per group)
+                    auto offs = [&](int l0) { return *reinterpret_cast<const u32x4 *>(ml + l0); };
+                    auto tfetch = [&](const u32x4 &o, f32x4 (&x)[4]) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f32x4 *>(tb + o[u]);
+                    };
                     int l = 0;
                     const int ng = n >> 2;  // whole groups
                     if (ng > 0) {
                         f32x4 xa[4], xb[4];
-                        fetch4(0, xa);
+                        u32x4 oa = offs(0), ob = offs(4);  // past the list: read, never used
+                        tfetch(oa, xa);
+                        oa = offs(8);
                         int g = 0;
                         for (; g + 2 < ng; g += 2) {
-                            fetch4(4 * (g + 1), xb);
+                            tfetch(ob, xb);
+                            ob = offs(4 * (g + 3));
                             group(xa);
-                            fetch4(4 * (g + 2), xa);
+                            tfetch(oa, xa);
+                            oa = offs(4 * (g + 4));
                             group(xb);
                         }
                         if (g + 1 < ng) {
-                            fetch4(4 * (g + 1), xb);
+                            tfetch(ob, xb);
                             group(xa);
                             group(xb);
                         } else {
