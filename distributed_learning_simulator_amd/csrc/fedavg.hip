@@ -244,51 +244,143 @@ struct UnionDiv {
     f32x4 c[DLS_SUBSET_UNION_MAX];
 };
 
-// The kernel: one block of kUnionWaves waves per CU, persistent over
-// 256-parameter tiles (a lane owns 4).  The tile's t_j of
-// the <= 64 union clients live in LDS, double-buffered: while the block computes
-// tile i from one buffer, each wave's loads of tile i+1's rows are in flight, and
-// after its coalitions it turns them into t_j in the other buffer — one barrier
-// per tile.  The S coalitions are dealt to the waves once per block, longest
-// first to the least loaded wave (a static LPT plan, so the per-tile barrier
-// waits for a balanced set); a wave holds its coalitions' results in registers
-// and stores them after staging the next tile, so its next loads never wait
-// behind its stores.  Per membership: one ds_read_b128 of t (4 parameters), the
-// quotient (2 ops two-constant / 3 Markstein, element pairs packed) and the add.
-// (With 50 coalitions the plan leaves two waves 4 coalitions and the rest 3: the
-// most loaded wave carries ~1.18 x the mean.  Measured and dropped: PAIRS of
-// tiles per barrier interval, 2S units (coalition, tile) dealt by the same LPT
-// (~1.08 x the mean), staging between two barriers — bit-identical and 1.4 %
-// slower, 1.818 vs 1.793 ms, profiles/r05_union_ab.txt: the barrier's wait
-// for the most loaded wave is not what bounds this kernel.  Its waves are parked
-// on s_waitcnt / the barrier 60 % of their cycles and issue VALU 14 % (x 4 waves
-// per SIMD: the SIMD's VALU ~56 % busy), same file; reading each group's member
-// offsets two groups ahead of its t reads took 1.5 % off.)
+// The kernel: TWO blocks of kUnionWaves = 8 waves per CU, persistent over
+// 256-parameter tiles (a lane owns 4), so that one block's barriers, staging and
+// load waits are filled by the other block's walks.  A block's LDS (< 80 KB) holds
+// one tile's t_j of the <= 64 union clients (64 KiB) and the member lists as
+// 16-bit offsets; per tile: walk the coalitions (each result stored as soon as
+// it is summed), barrier, turn the next tile's rows — loaded during the walk —
+// into t_j, issue the loads of the tile after, barrier.  The S coalitions are
+// dealt to the waves once per block, longest first to the least loaded wave (a
+// static LPT plan; 8 waves with ~6 coalitions each balance to ~1.05 x the mean).
+// Per membership: one ds_read_b128 of t (4 parameters), the quotient (2 ops
+// two-constant / 3 Markstein, element pairs packed) and the add.
+// (Round 5 history, profiles/r05_union_ab.txt: one 16-wave block per CU with a
+// double-buffered 128 KiB t took 1.77-1.79 ms at S = K = 50; its waves were
+// parked on s_waitcnt / the barrier 60 % of their cycles.  Pairs of tiles per
+// barrier interval in that kernel, for balance: 1.4 % slower; its member offsets
+// read two groups ahead: 1.5 % faster; this kernel: 3 % faster, 1.745 vs 1.80
+// ms.  Per membership it issues ~8 VALU instructions (the 6 packed ops, the t
+// address, the offset unpack): at ~53 % VALU busy on every SIMD, 1.3 ms would
+// take ~72 %.)
 //
 // f32x4 add as 2 v_pk_add_f32 (packed fp32 issues two lanes' elements at the
 // cost of one scalar op: tools/valu_rate_probe.hip measured 75 vs 38 T lane-op/s)
 __device__ __forceinline__ f32x4 addu(f32x4 a, f32x4 b) { return a + b; }
-constexpr int kUnionWaves = 16;
-constexpr int kUnionKMax = 8;   // coalitions per wave (the plan caps it; 16 x 8 >= 64)
-#ifndef DLS_UNION_AHEAD
-#define DLS_UNION_AHEAD 2
-#endif
-constexpr int kUnionAhead = DLS_UNION_AHEAD;  // tiles of client rows in flight (1 or 2)
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+constexpr int kUnionWaves = 8;
+constexpr int kUnionKMax = DLS_SUBSET_UNION_MAX / kUnionWaves;  // coalitions per wave (the plan caps it)
+constexpr int kUnionListRow = kUnionChunk + 8;  // + the offsets read ahead of a list's end
+
+// acc = fl(acc + fl(t_l / N)) over a coalition's members l < n, in order: t at
+// byte offset ml[l] from tb (this lane's 16 B of client 0); cc = the coalition's
+// UnionDiv constants.  tile_fast: every t of the tile is in the fast range.
+__device__ __forceinline__ f32x4 union_walk(f32x4 acc, const char *tb, const uint16_t *ml, int n, f32x4 cc,
+                                            bool tile_fast) {
+    auto tload = [&](int l) { return *reinterpret_cast<const f32x4 *>(tb + ml[l]); };
+    if (__builtin_expect(tile_fast, 1)) {
+        // the coalition's constants as SGPRs (pk ops take them with op_sel, no VGPR
+        // pair copies)
+        const float cy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.x)));
+        const float cl = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.y)));
+        const float cb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.z)));
+        const f32x2 y2 = f32x2{cy, cy}, l2 = f32x2{cl, cl};
+        const f32x2 b2 = f32x2{cb, cb};
+        // the division method is decided once per coalition (two copies of the
+        // member loop), not per member
+        auto walk = [&](auto two_c) {
+            constexpr bool TWO = decltype(two_c)::value;
+            auto quot = [&](f32x4 t) {
+                const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
+                f32x2 ql, qh;
+                if constexpr (TWO) {
+                    ql = __builtin_elementwise_fma(tl, y2, tl * l2);
+                    qh = __builtin_elementwise_fma(th, y2, th * l2);
+                } else {
+                    const f32x2 ql0 = tl * y2, qh0 = th * y2;
+                    ql = __builtin_elementwise_fma(__builtin_elementwise_fma(-ql0, b2, tl), y2, ql0);
+                    qh = __builtin_elementwise_fma(__builtin_elementwise_fma(-qh0, b2, th), y2, qh0);
+                }
+                return f32x4{ql.x, ql.y, qh.x, qh.y};
+            };
+            // groups of 4 members, ping-pong between two register sets (the next
+            // group's t are read from LDS while this group's 4 independent
+            // quotients are computed; no register rotation).  A group's 4 member
+            // offsets (one broadcast 8-byte read) are read two groups ahead of its
+            // t: the t reads depend on them, and read just before, their latency
+            // would stall the wave once per group.
+            auto offs = [&](int l0) { return *reinterpret_cast<const u32x2 *>(ml + l0); };
+            auto tfetch = [&](u32x2 o, f32x4 (&x)[4]) {
+                x[0] = *reinterpret_cast<const f32x4 *>(tb + (o.x & 0xffffu));
+                x[1] = *reinterpret_cast<const f32x4 *>(tb + (o.x >> 16));
+                x[2] = *reinterpret_cast<const f32x4 *>(tb + (o.y & 0xffffu));
+                x[3] = *reinterpret_cast<const f32x4 *>(tb + (o.y >> 16));
+            };
+            auto group = [&](const f32x4 (&x)[4]) {
+                const f32x4 q0 = quot(x[0]), q1 = quot(x[1]), q2 = quot(x[2]), q3 = quot(x[3]);
+                acc = addu(addu(addu(addu(acc, q0), q1), q2), q3);
+            };
+            int l = 0;
+            const int ng = n >> 2;  // whole groups
+            if (ng > 0) {
+                f32x4 xa[4], xb[4];
+                u32x2 oa = offs(0), ob = offs(4);  // past the list: read, never used
+                tfetch(oa, xa);
+                oa = offs(8);
+                int g = 0;
+                for (; g + 2 < ng; g += 2) {
+                    tfetch(ob, xb);
+                    ob = offs(4 * (g + 3));
+                    group(xa);
+                    tfetch(oa, xa);
+                    oa = offs(4 * (g + 4));
+                    group(xb);
+                }
+                if (g + 1 < ng) {
+                    tfetch(ob, xb);
+                    group(xa);
+                    group(xb);
+                } else {
+                    group(xa);
+                }
+                l = 4 * ng;
+            }
+            for (; l < n; ++l) acc = addu(acc, quot(tload(l)));
+        };
+        if ((__float_as_uint(cc.w) & 1u) != 0)  // wave-uniform
+            walk(std::true_type{});
+        else
+            walk(std::false_type{});
+    } else {  // zeros, denormals, huge values, inf / nan, divisors out of range
+        FastDiv d;
+        d.b = cc.z;
+        d.y = cc.x;
+        d.fast = (__float_as_uint(cc.w) & 2u) != 0;
+        for (int l = 0; l < n; ++l) {
+            const f32x4 t = tload(l);
+            for (int e = 0; e < 4; ++e)
+                acc[e] += (d.fast && in_fast_range(t[e])) ? markstein(t[e], d.b, d.y) : t[e] / d.b;
+        }
+    }
+    return acc;
+}
 
 template <bool ACC>
-__global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
+__global__ __launch_bounds__(64 * kUnionWaves, 4) void k_subset_union(
     const f32x4 *__restrict__ Uv, int64_t ldu4, const int32_t *__restrict__ urows,
     const float *__restrict__ uw, const uint64_t *__restrict__ member, int Ku, UnionDiv dv, int S,
     int64_t P4, int64_t ntiles, f32x4 *__restrict__ out, int64_t ldo4) {
     constexpr int W = kUnionWaves, NL = kUnionChunk / kUnionWaves;
-    __shared__ f32x4 ts[2][kUnionChunk * 64];                   // 2 x 64 KiB
-    // member byte offsets in a t buffer (client j: j * 1 KiB), per coalition; a
-    // wave reads 4 at a time as one broadcast ds_read_b128 (no readlane per member)
-    __shared__ __attribute__((aligned(16))) uint32_t lst[DLS_SUBSET_UNION_MAX][kUnionChunk + 8];  // + the offsets read ahead
-    __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];                 // UnionDiv, per coalition
+    static_assert(kUnionWaves * kUnionKMax >= DLS_SUBSET_UNION_MAX, "plan capacity");
+    __shared__ f32x4 ts[kUnionChunk * 64];  // 64 KiB: one tile's t
+    // member byte offsets in ts (client j: j * 1 KiB < 2^16), per coalition; a wave
+    // reads 4 at a time as one broadcast 8-byte read (no readlane per member)
+    __shared__ __attribute__((aligned(16))) uint16_t lst[DLS_SUBSET_UNION_MAX][kUnionListRow];
+    __shared__ f32x4 cst[DLS_SUBSET_UNION_MAX];  // UnionDiv, per coalition
     __shared__ int lens[DLS_SUBSET_UNION_MAX];
-    __shared__ int plan[W][kUnionKMax + 1];                        // [0] = count, then coalitions
-    __shared__ uint32_t tbad[2][W];
+    __shared__ int plan[W][kUnionKMax + 1];  // [0] = count, then coalitions
+    __shared__ uint32_t tbad[W];
+    const int64_t G = gridDim.x;
     int64_t tile = blockIdx.x;
     if (tile >= ntiles) return;  // block-uniform
     const int lane = __lane_id();
@@ -301,9 +393,8 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
     for (int c = wv; c < S; c += W) {
         const uint64_t in = __ballot((mj >> c) & 1ull);
         if ((mj >> c) & 1ull)
-            lst[c][__builtin_amdgcn_mbcnt_hi((uint32_t)(in >> 32),
-                                             __builtin_amdgcn_mbcnt_lo((uint32_t)in, 0u))] =
-                (uint32_t)lane << 10;
+            lst[c][__builtin_amdgcn_mbcnt_hi((uint32_t)(in >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)in, 0u))] =
+                (uint16_t)(lane << 10);
         if (lane == 0) {
             lens[c] = __popcll(in);
             cst[c] = dv.c[c];
@@ -330,11 +421,10 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             load[bw] += lens[best] + 2;  // + the coalition's fixed cost
         }
     }
-    // loader slots: wave wv stages clients wv + W l (l < NL) that exist; two
-    // register sets, so that the loads of the next TWO tiles are in flight while a
-    // tile is computed (kUnionAhead = 2; the LDS holds only two staged tiles)
-    f32x4 RA[NL], RB[NL];
-    auto issue = [&](int64_t t, f32x4 (&R)[NL]) {
+    // loader slots: wave wv stages clients wv + W l (l < NL) that exist; R holds
+    // the loads of the next tile while this one is walked
+    f32x4 R[NL];
+    auto issue = [&](int64_t t) {
         const int64_t i0 = t * 64 + lane;
         const int64_t iq = i0 < P4 ? i0 : P4 - 1;
 #pragma unroll
@@ -346,7 +436,7 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
             }
         }
     };
-    auto stage = [&](int b, const f32x4 (&R)[NL]) {  // t_j = fl(x_j * n_j) into buffer b; out-of-range flag
+    auto stage = [&]() {  // t_j = fl(x_j * n_j) into ts; out-of-range flag
         uint32_t bad = 0;
 #pragma unroll
         for (int l = 0; l < NL; ++l) {
@@ -358,19 +448,16 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
                 t.y = R[l].y * wk;
                 t.z = R[l].z * wk;
                 t.w = R[l].w * wk;
-                ts[b][j * 64 + lane] = t;
+                ts[j * 64 + lane] = t;
                 bad |= (uint32_t)(__ballot(!all_in_fast_range(t)) != 0);
             }
         }
-        if (lane == 0) tbad[b][wv] = bad;
+        if (lane == 0) tbad[wv] = bad;
     };
-    issue(tile, RA);
-    stage(0, RA);
-    if (kUnionAhead > 1) {
-        if (tile + gridDim.x < ntiles) issue(tile + gridDim.x, RA);
-        if (tile + 2 * (int64_t)gridDim.x < ntiles) issue(tile + 2 * (int64_t)gridDim.x, RB);
-    }
-    __syncthreads();  // buffer 0 and the plan are ready
+    issue(tile);
+    stage();
+    if (tile + G < ntiles) issue(tile + G);
+    __syncthreads();  // the first tile's t and the plan are ready
     const int nk = __builtin_amdgcn_readfirstlane(plan[wv][0]);
     int cid[kUnionKMax];
 #pragma unroll
@@ -379,145 +466,30 @@ __global__ __launch_bounds__(64 * kUnionWaves) void k_subset_union(
 #pragma unroll
     for (int k = 0; k < kUnionKMax; ++k)
         if (k < nk) fast &= (int)((__float_as_uint(cst[cid[k]].w) & 2u) != 0);
-    int b = 0;
-    // one tile: Rs holds the loads of the next tile (staged after the compute),
-    // then takes those of the tile after the one in flight in the other set
-    auto one_tile = [&](f32x4 (&Rs)[NL]) {
+    const char *tb = reinterpret_cast<const char *>(ts) + 16 * lane;
+    for (;;) {
         const int64_t i0 = tile * 64 + lane;
         const int64_t iq = i0 < P4 ? i0 : P4 - 1;
-        const int64_t next = tile + gridDim.x;
-        f32x4 res[kUnionKMax];
-#pragma unroll
-        for (int k = 0; k < kUnionKMax; ++k)
-            if (ACC && k < nk) res[k] = out[(int64_t)cid[k] * ldo4 + iq];
-        if (kUnionAhead == 1 && next < ntiles) issue(next, Rs);  // in flight during this tile's coalitions
         uint32_t anybad = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) anybad |= tbad[b][w];
+        for (int w = 0; w < W; ++w) anybad |= tbad[w];
         const bool tile_fast = fast && anybad == 0;
-        const char *tb = reinterpret_cast<const char *>(ts[b]) + 16 * lane;
 #pragma unroll
         for (int k = 0; k < kUnionKMax; ++k) {
             if (k >= nk) break;  // wave-uniform
             const int c = cid[k];
-            f32x4 acc = ACC ? res[k] : f32x4{-0.f, -0.f, -0.f, -0.f};
-            const f32x4 cc = cst[c];
-            const int n = lens[c];
-            const uint32_t *ml = lst[c];
-            auto tload = [&](int l) {
-                return *reinterpret_cast<const f32x4 *>(tb + ml[l]);
-            };
-            if (__builtin_expect(tile_fast, 1)) {
-                // the coalition's constants as SGPRs (pk ops take them with op_sel,
-                // no VGPR pair copies)
-                const float cy = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.x)));
-                const float cl = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.y)));
-                const float cb = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(cc.z)));
-                const f32x2 y2 = f32x2{cy, cy}, l2 = f32x2{cl, cl};
-                const f32x2 b2 = f32x2{cb, cb};
-                // the division method is decided once per coalition (two copies of
-                // the member loop), not per member
-                auto walk = [&](auto two_c) {
-                    constexpr bool TWO = decltype(two_c)::value;
-                    auto quot = [&](f32x4 t) {
-                        const f32x2 tl = f32x2{t.x, t.y}, th = f32x2{t.z, t.w};
-                        f32x2 ql, qh;
-                        if constexpr (TWO) {
-                            ql = __builtin_elementwise_fma(tl, y2, tl * l2);
-                            qh = __builtin_elementwise_fma(th, y2, th * l2);
-                        } else {
-                            const f32x2 ql0 = tl * y2, qh0 = th * y2;
-                            ql = __builtin_elementwise_fma(__builtin_elementwise_fma(-ql0, b2, tl),
-                                                           y2, ql0);
-                            qh = __builtin_elementwise_fma(__builtin_elementwise_fma(-qh0, b2, th),
-                                                           y2, qh0);
-                        }
-                        return f32x4{ql.x, ql.y, qh.x, qh.y};
-                    };
-                    // groups of 4 members, ping-pong between two register sets (the
-                    // next group's t are read from LDS while this group's 4
-                    // independent quotients are computed; no register rotation)
-                    auto group = [&](const f32x4 (&x)[4]) {
-                        const f32x4 q0 = quot(x[0]), q1 = quot(x[1]), q2 = quot(x[2]),
-                                    q3 = quot(x[3]);
-                        acc = addu(addu(addu(addu(acc, q0), q1), q2), q3);
-                    };
-                    // a group's 4 member offsets are read two groups ahead of its t
-                    // (the t reads depend on them: read just before, their latency
-                    // would stall the wave once per group)
-                    auto offs = [&](int l0) { return *reinterpret_cast<const u32x4 *>(ml + l0); };
-                    auto tfetch = [&](const u32x4 &o, f32x4 (&x)[4]) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f32x4 *>(tb + o[u]);
-                    };
-                    int l = 0;
-                    const int ng = n >> 2;  // whole groups
-                    if (ng > 0) {
-                        f32x4 xa[4], xb[4];
-                        u32x4 oa = offs(0), ob = offs(4);  // past the list: read, never used
-                        tfetch(oa, xa);
-                        oa = offs(8);
-                        int g = 0;
-                        for (; g + 2 < ng; g += 2) {
-                            tfetch(ob, xb);
-                            ob = offs(4 * (g + 3));
-                            group(xa);
-                            tfetch(oa, xa);
-                            oa = offs(4 * (g + 4));
-                            group(xb);
-                        }
-                        if (g + 1 < ng) {
-                            tfetch(ob, xb);
-                            group(xa);
-                            group(xb);
-                        } else {
-                            group(xa);
-                        }
-                        l = 4 * ng;
-                    }
-                    for (; l < n; ++l) acc = addu(acc, quot(tload(l)));
-                };
-                if ((__float_as_uint(cc.w) & 1u) != 0)  // wave-uniform
-                    walk(std::true_type{});
-                else
-                    walk(std::false_type{});
-            } else {  // zeros, denormals, huge values, inf / nan, divisors out of range
-                FastDiv d;
-                d.b = cc.z;
-                d.y = cc.x;
-                d.fast = (__float_as_uint(cc.w) & 2u) != 0;
-                for (int l = 0; l < n; ++l) {
-                    const f32x4 t = tload(l);
-                    for (int e = 0; e < 4; ++e)
-                        acc[e] += (d.fast && in_fast_range(t[e])) ? markstein(t[e], d.b, d.y)
-                                                                  : t[e] / d.b;
-                }
-            }
-            res[k] = acc;
+            f32x4 *dst = out + (int64_t)c * ldo4;
+            const f32x4 acc = union_walk(ACC ? dst[iq] : f32x4{-0.f, -0.f, -0.f, -0.f}, tb, lst[c], lens[c],
+                                         cst[c], tile_fast);
+            if (i0 < P4) dst[i0] = acc;
         }
-        if (next < ntiles) stage(b ^ 1, Rs);  // the next tile's t (its loads have landed by now)
-        if (kUnionAhead > 1 && next + 2 * (int64_t)gridDim.x < ntiles)
-            issue(next + 2 * (int64_t)gridDim.x, Rs);
-#pragma unroll
-        for (int k = 0; k < kUnionKMax; ++k)
-            if (k < nk && i0 < P4)
-                out[(int64_t)cid[k] * ldo4 + i0] = res[k];
-        __syncthreads();  // buffer b ^ 1 is complete; buffer b free for the tile after next
-    };
-    if (kUnionAhead == 1) {
-        for (; tile < ntiles; tile += gridDim.x, b ^= 1) one_tile(RA);
-    } else {
-        // the register sets alternate (a copy of an in-flight load's registers
-        // would wait for it), so the loop is unrolled by two
-        while (tile < ntiles) {
-            one_tile(RA);
-            tile += gridDim.x;
-            b ^= 1;
-            if (tile >= ntiles) break;
-            one_tile(RB);
-            tile += gridDim.x;
-            b ^= 1;
-        }
+        const int64_t next = tile + G;
+        if (next >= ntiles) break;  // block-uniform
+        __syncthreads();  // every wave is done with this tile's t
+        stage();           // the next tile's (its loads have landed by now)
+        if (next + G < ntiles) issue(next + G);
+        __syncthreads();
+        tile = next;
     }
 }
 
