@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-end rehearsal on one GPU box: the GPU suite, smoke(), the default bench,
-# and a rocprofv3 kernel trace of the utility evaluation's convolutions.
+# a rocprofv3 kernel trace of the utility evaluation's convolutions, and one of
+# the default bench (stats over all launches + each kernel's last 10 launches).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
@@ -14,3 +15,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D" -
 { head -1 "$D/run_kernel_stats.csv"; grep "dls::" "$D/run_kernel_stats.csv" || true; } > "$OUT/conv_kernel_stats.csv"
 rm -rf "$D"
 echo "conv trace: $OUT/conv_kernel_stats.csv"
+D2="$(mktemp -d /tmp/benchtrace.XXXXXX)"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D2" -o run -- \
+    python3 -u "$ROOT/bench.py" > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err" || exit $?
+cd "$ROOT"
+cp "$D2/run_kernel_stats.csv" "$OUT/kernel_stats_all.csv"
+{ head -1 "$D2/run_kernel_trace.csv"; grep "dls::" "$D2/run_kernel_trace.csv" || true; } > "$D2/kernel_trace_dls.csv"
+python3 tools/trace_summary.py "$OUT/kernel_stats_all.csv" > "$OUT/kernel_stats_all.txt"
+python3 tools/trace_summary.py --tail 10 "$D2/kernel_trace_dls.csv" > "$OUT/kernel_tail10_all.txt"
+rm -rf "$D2"
+echo "bench trace: $OUT/kernel_stats_all.txt $OUT/kernel_tail10_all.txt"
