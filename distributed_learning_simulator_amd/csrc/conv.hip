@@ -118,6 +118,24 @@ __device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, co
     }
 }
 
+// One k-step's fragments (16 channels): A hi / lo of the wave's two channel
+// tiles, B hi / lo of its two pixel tiles; mfma_frag takes mfma_chunk's products
+// in mfma_chunk's order
+struct Frag {
+    bf16x8 ah[2], al[2], bh[2], bl[2];
+};
+
+__device__ __forceinline__ void mfma_frag(WaveAcc &acc, const Frag &f) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
+        }
+}
+
 __device__ __forceinline__ void zero_acc(WaveAcc &acc) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -469,31 +487,41 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 // thread gathers its output pixel's inputs straight from the fp32 NCHW image
 // batch (k = (ky * KW + kx) * C + ci, zero outside the image and past the 27),
 // splits them and writes the pixel's B row to LDS — then one chunk of MFMAs and
-// the LDS epilogue.  Weights: dls_conv_pack_weights_im2col_f32 with Kp = kBK.
+// the epilogue.  Weights: dls_conv_pack_weights_im2col_f32 with Kp = kBK.
 // CIN / KHW > 0: the input channels and the (square) kernel size as constants
 // (the index arithmetic of the 27-term gather folds away); 0: runtime a.C / a.KW.
+// LDS is what bounds its occupancy (a short block: gather, 24 MFMAs, epilogue),
+// so each wave loads its A fragments straight from the weights (16 B per lane
+// and fragment, L2-resident) and the epilogue transposes 32 channels at a time:
+// 37 KB per block, 4 blocks per CU (the LDS-staged weights and one 64-channel
+// epilogue pass: 70 KB, 2 blocks).  The same products in the same order and the
+// same epilogue arithmetic: the same bits.
 template <int WPIX, int CIN = 0, int KHW = 0>
 __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float *__restrict__ x) {
-    constexpr int NT = 64 * WPIX, BMC = kWaveTile, BNP = kWaveTile * WPIX;
-    constexpr int PPR = kBK / 4, HP = kBK / 8, RPP = NT / PPR, NA = BMC / RPP;
-    constexpr int STAGE = (BMC + BNP) * kRowB;
-    constexpr int EPI = BNP * (4 * BMC + 16);
+    constexpr int NT = 64 * WPIX, BNP = kWaveTile * WPIX;
+    constexpr int STAGE = BNP * kRowB;
+    constexpr int SLAB = 32;                  // channels per epilogue pass
+    constexpr int EROW = 4 * SLAB + 16;
+    constexpr int EPI = BNP * EROW;
     static_assert(NT == BNP, "one pixel row per thread");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
-    uint8_t *As = smem, *Bs = smem + BMC * kRowB;
+    uint8_t *Bs = smem;
     const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
     const int t = tile_of_block();
-    const int co0 = (t % a.co_tiles) * BMC;
+    const int co0 = (t % a.co_tiles) * kWaveTile;
     const int pix0 = (t / a.co_tiles) * BNP;
-    // weights: piece `part` of rows tid / PPR + RPP * u
-    const int part = tid % PPR, row0 = tid / PPR;
+    // A fragments of both k-steps (in flight during the gather): channel tile i,
+    // lane row co0 + 32 i + r, k = 16 s + 8 h .. + 7 (hi), + K (lo)
+    Frag f[kBK / 16];
 #pragma unroll
-    for (int u = 0; u < NA; ++u) {
-        const int row = row0 + RPP * u;
-        const int wo = part < HP ? part * 8 : a.K + (part - HP) * 8;
-        *reinterpret_cast<u32x4 *>(As + row * kRowB + part * 16) =
-            *reinterpret_cast<const u32x4 *>(a.w + (int64_t)(co0 + row) * (2 * a.K) + wo);
-    }
+    for (int s = 0; s < kBK / 16; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint16_t *wr = a.w + (int64_t)(co0 + 32 * i + r) * (2 * a.K) + 16 * s + 8 * h;
+            f[s].ah[i] = *reinterpret_cast<const bf16x8 *>(wr);
+            f[s].al[i] = *reinterpret_cast<const bf16x8 *>(wr + a.K);
+        }
     // this thread's pixel: gather, split, one LDS row
     {
         const int p = pix0 + tid;
@@ -533,11 +561,68 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
     __syncthreads();
     WaveAcc acc;
     zero_acc(acc);
-    const int r = lane & 31, h = lane >> 5;
-    const uint8_t *b0 = Bs + (wp * kWaveTile + r) * kRowB;
-    mfma_chunk(acc, As + r * kRowB, b0, b0 + 32 * kRowB, h);
-    __syncthreads();  // the epilogue reuses the operands' LDS
-    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, 0, wp, tid);
+    const uint8_t *b0 = Bs + (wp * kWaveTile + r) * kRowB, *b1 = b0 + 32 * kRowB;
+#pragma unroll
+    for (int s = 0; s < kBK / 16; ++s) {  // mfma_chunk's order: k-step, then tiles
+        const int off = 32 * s + 16 * h;
+        f[s].bh[0] = *reinterpret_cast<const bf16x8 *>(b0 + off);
+        f[s].bl[0] = *reinterpret_cast<const bf16x8 *>(b0 + 2 * kBK + off);
+        f[s].bh[1] = *reinterpret_cast<const bf16x8 *>(b1 + off);
+        f[s].bl[1] = *reinterpret_cast<const bf16x8 *>(b1 + 2 * kBK + off);
+        mfma_frag(acc, f[s]);
+    }
+    // epilogue, one 32-channel slab (channel tile i) per pass: epilogue_lds's
+    // arithmetic (batch norm, ReLU, split; the stem has no residual)
+    constexpr int GPP = SLAB / 8, NPC = BNP * GPP / NT;
+    static_assert(NT % GPP == 0 && (BNP * GPP) % NT == 0, "epilogue shape");
+    const int cl = 8 * (tid % GPP);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        __syncthreads();  // the operands' / the previous slab's LDS is free
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int pl = wp * kWaveTile + 32 * j + r;
+                *reinterpret_cast<f32x4 *>(smem + pl * EROW + (8 * g + 4 * h) * 4) =
+                    f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+            }
+        __syncthreads();
+        const int co = co0 + SLAB * i + cl;
+        float m[8], iv[8], wv[8], bv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            m[e] = a.consts ? a.consts[co + e] : 0.f;
+            iv[e] = a.consts ? a.consts[a.Cout + co + e] : 1.f;
+            wv[e] = a.consts ? a.consts[2 * a.Cout + co + e] : 1.f;
+            bv[e] = a.consts ? a.consts[3 * a.Cout + co + e] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < NPC; ++u) {
+            const int pl = (tid + NT * u) / GPP;
+            const int p = pix0 + pl;
+            if (p >= a.M) continue;
+            const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4);
+            const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4 + 16);
+            float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            if (a.consts) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
+            }
+            uint32_t hi[8], lo[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float xv = v[e];
+                if (a.relu) xv = xv > 0.f ? xv : (xv == xv ? 0.f : xv);  // relu keeps NaN, as torch
+                split2(xv, hi[e], lo[e]);
+            }
+            const int64_t ob = (int64_t)p * (2 * a.Cout) + co;
+            *reinterpret_cast<u32x4 *>(a.y + ob) =
+                u32x4{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
+            *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) =
+                u32x4{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+        }
+    }
 }
 
 // fp32 NCHW image batch -> split NHWC with Cp >= C channels (zeros beyond C)
