@@ -145,76 +145,88 @@ __device__ __forceinline__ void zero_acc(WaveAcc &acc) {
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 }
 
-// Epilogue through LDS (smem >= BNP * (4 BMC + 16) bytes, free: every wave past
-// its last read of the staged operands): the raw tiles are transposed to
-// [pixel][channel] fp32, then each thread takes 8 channels of a pixel — batch norm
-// fma(w, (x - mean) * iv, b), + residual (hi + lo), ReLU, split — and stores 16-B
-// hi and lo pieces: a block's threads write whole runs of its pixels' rows.
+// Epilogue through LDS (smem >= BNP * (4 BMC / NPASS + 16) bytes, free: every
+// wave past its last read of the staged operands): the raw tiles are transposed
+// to [pixel][channel] fp32, then each thread takes 8 channels of a pixel — batch
+// norm fma(w, (x - mean) * iv, b), + residual (hi + lo), ReLU, split — and stores
+// 16-B hi and lo pieces: a block's threads write whole runs of its pixels' rows.
 // Lane (r, h) of wave (wc, wp) holds pixel wp*64 + 32 j + r, channels
-// wc*64 + 32 i + 8 g + 4 h + e in acc[i][j][4 g + e].
-template <int BMC, int BNP, int NT>
+// wc*64 + 32 i + 8 g + 4 h + e in acc[i][j][4 g + e].  NPASS = 2 transposes one
+// 32-channel tile i of every wave per pass (half the LDS; the same arithmetic
+// per element): pass p's local channel lc is channel (lc / 32) * 64 + 32 p +
+// lc % 32 of the block.
+template <int BMC, int BNP, int NT, int NPASS = 1>
 __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, const ConvArgs &a,
                                              int co0, int pix0, int wc, int wp, int tid) {
-    constexpr int EROW = 4 * BMC + 16;
-    const int lane = tid & 63, r = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int pl = wp * kWaveTile + 32 * j + r;
-                const int cl = wc * kWaveTile + 32 * i + 8 * g + 4 * h;
-                *reinterpret_cast<f32x4 *>(smem + pl * EROW + cl * 4) =
-                    f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-            }
-    __syncthreads();
-    constexpr int GPP = BMC / 8;  // 8-channel groups per pixel
+    static_assert(NPASS == 1 || NPASS == 2, "epilogue passes");
+    constexpr int SLAB = BMC / NPASS;  // channels per pass
+    constexpr int EROW = 4 * SLAB + 16;
+    constexpr int GPP = SLAB / 8;      // 8-channel groups per pixel
     constexpr int NPC = BNP * GPP / NT;
     static_assert(NT % GPP == 0 && (BNP * GPP) % NT == 0, "epilogue shape");
-    const int cl = 8 * (tid % GPP), co = co0 + cl;  // a thread's channel group is fixed
-    float m[8], iv[8], wv[8], bv[8];
+    const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int lc = 8 * (tid % GPP);  // a thread's channel group is fixed per pass
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        m[e] = a.consts ? a.consts[co + e] : 0.f;
-        iv[e] = a.consts ? a.consts[a.Cout + co + e] : 1.f;
-        wv[e] = a.consts ? a.consts[2 * a.Cout + co + e] : 1.f;
-        bv[e] = a.consts ? a.consts[3 * a.Cout + co + e] : 0.f;
-    }
-#pragma unroll 2
-    for (int u = 0; u < NPC; ++u) {
-        const int pl = (tid + NT * u) / GPP;
-        const int p = pix0 + pl;
-        if (p >= a.M) continue;
-        const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4);
-        const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4 + 16);
-        float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        const int64_t ob = (int64_t)p * (2 * a.Cout) + co;
-        if (a.consts) {
+    for (int p = 0; p < NPASS; ++p) {
+        if (p > 0) __syncthreads();  // the previous pass's reads are done
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
-        }
-        if (a.res) {
-            const u32x4 rh = *reinterpret_cast<const u32x4 *>(a.res + ob);
-            const u32x4 rl = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const uint32_t sh = 16 * (e & 1);
-                v[e] = v[e] + (bf16_to_f32((rh[e >> 1] >> sh) & 0xffffu) +
-                               bf16_to_f32((rl[e >> 1] >> sh) & 0xffffu));
+            for (int i = 0; i < 2; ++i) {
+                if (NPASS == 2 && i != p) continue;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int pl = wp * kWaveTile + 32 * j + r;
+                    const int cl = NPASS == 1 ? wc * kWaveTile + 32 * i + 8 * g + 4 * h : wc * 32 + 8 * g + 4 * h;
+                    *reinterpret_cast<f32x4 *>(smem + pl * EROW + cl * 4) =
+                        f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                }
             }
-        }
-        uint32_t hi[8], lo[8];
+        __syncthreads();
+        const int co = co0 + (NPASS == 1 ? lc : (lc / 32) * kWaveTile + 32 * p + lc % 32);
+        float m[8], iv[8], wv[8], bv[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            float x = v[e];
-            if (a.relu) x = x > 0.f ? x : (x == x ? 0.f : x);  // relu keeps NaN, as torch
-            split2(x, hi[e], lo[e]);
+            m[e] = a.consts ? a.consts[co + e] : 0.f;
+            iv[e] = a.consts ? a.consts[a.Cout + co + e] : 1.f;
+            wv[e] = a.consts ? a.consts[2 * a.Cout + co + e] : 1.f;
+            bv[e] = a.consts ? a.consts[3 * a.Cout + co + e] : 0.f;
         }
-        *reinterpret_cast<u32x4 *>(a.y + ob) =
-            u32x4{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
-        *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) =
-            u32x4{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+#pragma unroll 2
+        for (int u = 0; u < NPC; ++u) {
+            const int pl = (tid + NT * u) / GPP;
+            const int px = pix0 + pl;
+            if (px >= a.M) continue;
+            const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4);
+            const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4 + 16);
+            float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            const int64_t ob = (int64_t)px * (2 * a.Cout) + co;
+            if (a.consts) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
+            }
+            if (a.res) {
+                const u32x4 rh = *reinterpret_cast<const u32x4 *>(a.res + ob);
+                const u32x4 rl = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t sh = 16 * (e & 1);
+                    v[e] = v[e] + (bf16_to_f32((rh[e >> 1] >> sh) & 0xffffu) +
+                                   bf16_to_f32((rl[e >> 1] >> sh) & 0xffffu));
+                }
+            }
+            uint32_t hi[8], lo[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float x = v[e];
+                if (a.relu) x = x > 0.f ? x : (x == x ? 0.f : x);  // relu keeps NaN, as torch
+                split2(x, hi[e], lo[e]);
+            }
+            *reinterpret_cast<u32x4 *>(a.y + ob) =
+                u32x4{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
+            *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) =
+                u32x4{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+        }
     }
 }
 
@@ -230,8 +242,9 @@ __device__ __forceinline__ int tile_of_block() {
 // Any stride / padding / kernel size: every chunk stages the A rows (channels x
 // kBK) and the B rows (each output pixel's input pixel under the chunk's tap,
 // zero outside the image) through double-buffered LDS, register-staged.
-template <int WCO, int WPIX>
+template <int WCO, int WPIX, int NBUF = 2, int NPASS = 1>
 __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
+    static_assert(NBUF == 1 || NBUF == 2, "staging buffers");
     constexpr int NT = 64 * WCO * WPIX;
     constexpr int BMC = kWaveTile * WCO;   // output channels per block
     constexpr int BNP = kWaveTile * WPIX;  // pixels per block
@@ -239,8 +252,8 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
     constexpr int HP = kBK / 8;            // of which hi
     constexpr int RPP = NT / PPR;          // rows per staging pass
     constexpr int NA = BMC / RPP, NB = BNP / RPP;
-    constexpr int STAGE = 2 * (BMC + BNP) * kRowB;
-    constexpr int EPI = BNP * (4 * BMC + 16);
+    constexpr int STAGE = NBUF * (BMC + BNP) * kRowB;
+    constexpr int EPI = BNP * (4 * BMC / NPASS + 16);
     static_assert(NT % PPR == 0 && BMC % RPP == 0 && BNP % RPP == 0, "staging shape");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
 
@@ -316,13 +329,14 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
     for (int c = 0; c < nchunks; ++c) {
         const bool more = c + 1 < nchunks;
         if (more) load(c + 1);
-        const uint8_t *base = smem + (c & 1) * (BMC + BNP) * kRowB;
+        const uint8_t *base = smem + (NBUF == 2 ? (c & 1) : 0) * (BMC + BNP) * kRowB;
         const uint8_t *b0 = base + (BMC + wp * kWaveTile + r) * kRowB;
         mfma_chunk(acc, base + (wc * kWaveTile + r) * kRowB, b0, b0 + 32 * kRowB, h);
-        if (more) store((c + 1) & 1);
+        if (NBUF == 1 && more) __syncthreads();  // every wave is done with the buffer
+        if (more) store(NBUF == 2 ? (c + 1) & 1 : 0);
         __syncthreads();
     }
-    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
+    epilogue_lds<BMC, BNP, NT, NPASS>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
 // ------------------------------------------------------ 3x3, stride 1, pad 1
@@ -500,9 +514,7 @@ template <int WPIX, int CIN = 0, int KHW = 0>
 __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float *__restrict__ x) {
     constexpr int NT = 64 * WPIX, BNP = kWaveTile * WPIX;
     constexpr int STAGE = BNP * kRowB;
-    constexpr int SLAB = 32;                  // channels per epilogue pass
-    constexpr int EROW = 4 * SLAB + 16;
-    constexpr int EPI = BNP * EROW;
+    constexpr int EPI = BNP * (4 * kWaveTile / 2 + 16);  // two epilogue passes
     static_assert(NT == BNP, "one pixel row per thread");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *Bs = smem;
@@ -571,58 +583,8 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
         f[s].bl[1] = *reinterpret_cast<const bf16x8 *>(b1 + 2 * kBK + off);
         mfma_frag(acc, f[s]);
     }
-    // epilogue, one 32-channel slab (channel tile i) per pass: epilogue_lds's
-    // arithmetic (batch norm, ReLU, split; the stem has no residual)
-    constexpr int GPP = SLAB / 8, NPC = BNP * GPP / NT;
-    static_assert(NT % GPP == 0 && (BNP * GPP) % NT == 0, "epilogue shape");
-    const int cl = 8 * (tid % GPP);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        __syncthreads();  // the operands' / the previous slab's LDS is free
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int pl = wp * kWaveTile + 32 * j + r;
-                *reinterpret_cast<f32x4 *>(smem + pl * EROW + (8 * g + 4 * h) * 4) =
-                    f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-            }
-        __syncthreads();
-        const int co = co0 + SLAB * i + cl;
-        float m[8], iv[8], wv[8], bv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            m[e] = a.consts ? a.consts[co + e] : 0.f;
-            iv[e] = a.consts ? a.consts[a.Cout + co + e] : 1.f;
-            wv[e] = a.consts ? a.consts[2 * a.Cout + co + e] : 1.f;
-            bv[e] = a.consts ? a.consts[3 * a.Cout + co + e] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < NPC; ++u) {
-            const int pl = (tid + NT * u) / GPP;
-            const int p = pix0 + pl;
-            if (p >= a.M) continue;
-            const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4);
-            const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + cl * 4 + 16);
-            float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-            if (a.consts) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
-            }
-            uint32_t hi[8], lo[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float xv = v[e];
-                if (a.relu) xv = xv > 0.f ? xv : (xv == xv ? 0.f : xv);  // relu keeps NaN, as torch
-                split2(xv, hi[e], lo[e]);
-            }
-            const int64_t ob = (int64_t)p * (2 * a.Cout) + co;
-            *reinterpret_cast<u32x4 *>(a.y + ob) =
-                u32x4{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
-            *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) =
-                u32x4{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
-        }
-    }
+    __syncthreads();  // the epilogue reuses the operands' LDS
+    epilogue_lds<kWaveTile, BNP, NT, 2>(acc, smem, a, co0, pix0, 0, wp, tid);
 }
 
 // fp32 NCHW image batch -> split NHWC with Cp >= C channels (zeros beyond C)
@@ -722,8 +684,17 @@ __global__ __launch_bounds__(kPoolBlock) void k_pool_linear(const uint16_t *__re
     }
 }
 
+// The generic kernel's LDS form: 64-channel tiles (WCO = 1: 64 x 256 blocks)
+// stage through one buffer (two barriers per chunk) and transpose their epilogue
+// in two 32-channel passes, 46 instead of 92 KB per block (3 blocks per CU
+// instead of 1): the 32 -> 64-channel 1x1 convolution over the stem's im2col
+// 223 -> 153 us per 1000 images.  The 128-channel tiles keep double-buffered
+// staging and one epilogue pass (74 KB, 2 blocks per CU): their lean form,
+// 37 KB and 4 blocks per CU, made the stride-2 3x3 convolutions 2-3.5 % slower
+// (profiles/r05_conv_probe.txt r05g)
 template <int WCO, int WPIX>
 int launch_conv(ConvArgs a, hipStream_t st) {
+    constexpr int NBUF = WCO == 1 ? 1 : 2, NPASS = WCO == 1 ? 2 : 1;
     a.pix_tiles = (a.M + kWaveTile * WPIX - 1) / (kWaveTile * WPIX);
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
@@ -731,7 +702,8 @@ int launch_conv(ConvArgs a, hipStream_t st) {
         set_error("dls_conv_bn_act_split: %lld blocks", (long long)blocks);
         return DLS_EINVAL;
     }
-    hipLaunchKernelGGL((k_conv_bf16x3<WCO, WPIX>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0, st, a);
+    hipLaunchKernelGGL((k_conv_bf16x3<WCO, WPIX, NBUF, NPASS>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
+                       st, a);
     return check_launch("dls_conv_bn_act_split");
 }
 
