@@ -241,7 +241,9 @@ __device__ __forceinline__ int tile_of_block() {
 // ---------------------------------------------------------------- generic
 // Any stride / padding / kernel size: every chunk stages the A rows (channels x
 // kBK) and the B rows (each output pixel's input pixel under the chunk's tap,
-// zero outside the image) through double-buffered LDS, register-staged.
+// zero outside the image) through LDS, register-staged: double-buffered (NBUF =
+// 2, one barrier per chunk) or one buffer (NBUF = 1, two barriers per chunk, half
+// the LDS); NPASS: the epilogue's channel passes (epilogue_lds).
 template <int WCO, int WPIX, int NBUF = 2, int NPASS = 1>
 __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
     static_assert(NBUF == 1 || NBUF == 2, "staging buffers");
