@@ -262,7 +262,9 @@ struct UnionDiv {
 // read two groups ahead: 1.5 % faster; this kernel: 3 % faster, 1.745 vs 1.80
 // ms.  Per membership it issues ~8 VALU instructions (the 6 packed ops, the t
 // address, the offset unpack): at ~53 % VALU busy on every SIMD, 1.3 ms would
-// take ~72 %.)
+// take ~72 %.  Half-width tiles (2 parameters per lane: 32 KiB of t, 3 blocks
+// and 24 waves per CU, 73 VGPRs): bit-identical and 1 % slower, 1.739 vs 1.722
+// ms — more waves to hide the waits do not pay for the extra instructions.)
 //
 // f32x4 add as 2 v_pk_add_f32 (packed fp32 issues two lanes' elements at the
 // cost of one scalar op: tools/valu_rate_probe.hip measured 75 vs 38 T lane-op/s)
