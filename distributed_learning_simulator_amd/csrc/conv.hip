@@ -71,6 +71,23 @@ __device__ __forceinline__ void split2(float x, uint32_t &hi, uint32_t &lo) {
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
 
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// split2 of an element pair, packed: hi2 / lo2 hold a's bf16 in the low and b's
+// in the high half.  The conversions are gfx950's v_cvt_pk_bf16_f32, which is
+// bf16_rne bit for bit on all 2^32 fp32 patterns, NaN payloads included
+// (tools/bf16_cvt_probe.hip, profiles/r05_bf16_cvt_probe.txt): the same bits as
+// two split2 calls in a fifth of the instructions.
+__device__ __forceinline__ void split2x2(float a, float b, uint32_t &hi2, uint32_t &lo2) {
+    hi2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+    float ra = a - __uint_as_float(hi2 << 16);
+    float rb = b - __uint_as_float(hi2 & 0xffff0000u);
+    ra = (__float_as_uint(a) & 0x7f800000u) == 0x7f800000u ? 0.f : ra;
+    rb = (__float_as_uint(b) & 0x7f800000u) == 0x7f800000u ? 0.f : rb;
+    lo2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{ra, rb}, bf16x2));
+}
+
 struct ConvArgs {
     const uint16_t *x;      // split NHWC input [B][H][W][2C]
     const uint16_t *w;      // split weights [Cout][2K]
@@ -215,17 +232,15 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
                                    bf16_to_f32((rl[e >> 1] >> sh) & 0xffffu));
                 }
             }
-            uint32_t hi[8], lo[8];
+            if (a.relu) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float x = v[e];
-                if (a.relu) x = x > 0.f ? x : (x == x ? 0.f : x);  // relu keeps NaN, as torch
-                split2(x, hi[e], lo[e]);
+                for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : (v[e] == v[e] ? 0.f : v[e]);  // keeps NaN, as torch
             }
-            *reinterpret_cast<u32x4 *>(a.y + ob) =
-                u32x4{hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
-            *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) =
-                u32x4{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+            uint32_t hi[4], lo[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) split2x2(v[2 * q], v[2 * q + 1], hi[q], lo[q]);
+            *reinterpret_cast<u32x4 *>(a.y + ob) = u32x4{hi[0], hi[1], hi[2], hi[3]};
+            *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) = u32x4{lo[0], lo[1], lo[2], lo[3]};
         }
     }
 }
@@ -548,8 +563,7 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
             const int oy = rem / a.Wo, ox = rem - oy * a.Wo;
             const int C = CIN > 0 ? CIN : a.C, KW = KHW > 0 ? KHW : a.KW;
             const int nk = CIN > 0 ? CIN * KHW * KHW : a.taps * a.C;
-#pragma unroll
-            for (int k = 0; k < kBK; ++k) {
+            auto gather = [&](int k) {
                 float v = 0.f;
                 if (k < nk) {
                     const int tap = k / C, ci = k - tap * C;
@@ -558,11 +572,10 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
                     if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
                         v = x[(((int64_t)b * C + ci) * a.H + iy) * a.W + ix];
                 }
-                uint32_t hi, lo;
-                split2(v, hi, lo);
-                hw[k >> 1] |= hi << (16 * (k & 1));
-                lw[k >> 1] |= lo << (16 * (k & 1));
-            }
+                return v;
+            };
+#pragma unroll
+            for (int q = 0; q < kBK / 2; ++q) split2x2(gather(2 * q), gather(2 * q + 1), hw[q], lw[q]);
         }
 #pragma unroll
         for (int q = 0; q < kBK / 8; ++q) {
