@@ -232,9 +232,9 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
                                    bf16_to_f32((rl[e >> 1] >> sh) & 0xffffu));
                 }
             }
-            if (a.relu) {
+            if (a.relu) {  // keeps NaN, as torch; one select per element (no branches)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : (v[e] == v[e] ? 0.f : v[e]);  // keeps NaN, as torch
+                for (int e = 0; e < 8; ++e) v[e] = ((v[e] > 0.f) | (v[e] != v[e])) ? v[e] : 0.f;
             }
             uint32_t hi[4], lo[4];
 #pragma unroll
