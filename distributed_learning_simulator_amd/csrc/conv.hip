@@ -201,13 +201,24 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
             }
         __syncthreads();
         const int co = co0 + (NPASS == 1 ? lc : (lc / 32) * kWaveTile + 32 * p + lc % 32);
-        float m[8], iv[8], wv[8], bv[8];
+        // the 8 channels' batch-norm constants as element pairs: 8 vector loads
+        f32x2 m2[4], iv2[4], wv2[4], bv2[4];
+        if (a.consts) {
+            const f32x4 *c4[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            m[e] = a.consts ? a.consts[co + e] : 0.f;
-            iv[e] = a.consts ? a.consts[a.Cout + co + e] : 1.f;
-            wv[e] = a.consts ? a.consts[2 * a.Cout + co + e] : 1.f;
-            bv[e] = a.consts ? a.consts[3 * a.Cout + co + e] : 0.f;
+            for (int t = 0; t < 4; ++t) c4[t] = reinterpret_cast<const f32x4 *>(a.consts + t * a.Cout + co);
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const f32x4 cm = c4[0][hh], ci = c4[1][hh], cw = c4[2][hh], cb = c4[3][hh];
+                m2[2 * hh] = f32x2{cm[0], cm[1]};
+                m2[2 * hh + 1] = f32x2{cm[2], cm[3]};
+                iv2[2 * hh] = f32x2{ci[0], ci[1]};
+                iv2[2 * hh + 1] = f32x2{ci[2], ci[3]};
+                wv2[2 * hh] = f32x2{cw[0], cw[1]};
+                wv2[2 * hh + 1] = f32x2{cw[2], cw[3]};
+                bv2[2 * hh] = f32x2{cb[0], cb[1]};
+                bv2[2 * hh + 1] = f32x2{cb[2], cb[3]};
+            }
         }
 #pragma unroll 2
         for (int u = 0; u < NPC; ++u) {
@@ -216,22 +227,21 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
             if (px >= a.M) continue;
             const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4);
             const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4 + 16);
-            float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            f32x2 v2[4] = {f32x2{v0[0], v0[1]}, f32x2{v0[2], v0[3]}, f32x2{v1[0], v1[1]}, f32x2{v1[2], v1[3]}};
             const int64_t ob = (int64_t)px * (2 * a.Cout) + co;
-            if (a.consts) {
+            if (a.consts) {  // fma(w, (x - mean) * iv, b), element pairs on packed fp32
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = __builtin_fmaf(wv[e], (v[e] - m[e]) * iv[e], bv[e]);
+                for (int q = 0; q < 4; ++q) v2[q] = __builtin_elementwise_fma(wv2[q], (v2[q] - m2[q]) * iv2[q], bv2[q]);
             }
-            if (a.res) {
+            if (a.res) {  // + (hi + lo)
                 const u32x4 rh = *reinterpret_cast<const u32x4 *>(a.res + ob);
                 const u32x4 rl = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const uint32_t sh = 16 * (e & 1);
-                    v[e] = v[e] + (bf16_to_f32((rh[e >> 1] >> sh) & 0xffffu) +
-                                   bf16_to_f32((rl[e >> 1] >> sh) & 0xffffu));
-                }
+                for (int q = 0; q < 4; ++q)
+                    v2[q] = v2[q] + (f32x2{__uint_as_float(rh[q] << 16), __uint_as_float(rh[q] & 0xffff0000u)} +
+                                     f32x2{__uint_as_float(rl[q] << 16), __uint_as_float(rl[q] & 0xffff0000u)});
             }
+            float v[8] = {v2[0].x, v2[0].y, v2[1].x, v2[1].y, v2[2].x, v2[2].y, v2[3].x, v2[3].y};
             if (a.relu) {  // keeps NaN, as torch; one select per element (no branches)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) v[e] = ((v[e] > 0.f) | (v[e] != v[e])) ? v[e] : 0.f;
