@@ -268,7 +268,10 @@ __device__ __forceinline__ int tile_of_block() {
 // kBK) and the B rows (each output pixel's input pixel under the chunk's tap,
 // zero outside the image) through LDS, register-staged: double-buffered (NBUF =
 // 2, one barrier per chunk) or one buffer (NBUF = 1, two barriers per chunk, half
-// the LDS); NPASS: the epilogue's channel passes (epilogue_lds).
+// the LDS); NPASS: the epilogue's channel passes (epilogue_lds).  (Measured and
+// dropped: two register sets, each chunk's loads issued two chunks ahead —
+// 196 VGPRs, bit-identical, the stride-2 and 1x1 convolutions 45-60 % slower,
+// profiles/r05_conv_probe.txt r05c5.)
 template <int WCO, int WPIX, int NBUF = 2, int NPASS = 1>
 __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
     static_assert(NBUF == 1 || NBUF == 2, "staging buffers");
