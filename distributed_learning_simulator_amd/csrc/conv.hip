@@ -394,7 +394,9 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // the 64-channel layers (78 KB, still two blocks per CU) so that each wave reads
 // the next tap's first k-step fragments before the barrier and resumes its MFMAs
 // right after it (layer1 -0.1 to -0.6 %: the barrier's restart latency is not what
-// bounds it).  What does bound it (the same file,
+// bounds it); branch-free halo staging (every lane loading, padding rows from
+// pixel 0 then zeroed; stores unconditional): 2-10 % slower, the loads cost more
+// than the branches (r05c6).  What does bound it (the same file,
 // r05x2): with one bf16 product per k-step instead of three the layers take
 // 65-85 % of their time — the staging, the fragments' LDS reads and the barriers
 // barely overlap the MFMAs at two waves per SIMD.
