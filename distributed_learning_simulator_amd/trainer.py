@@ -105,7 +105,7 @@ class Inferencer:
     differ it runs the module's forward).  ``fused_eval=False`` always runs the
     module's forward."""
 
-    SPLIT_MIN_BATCH = 2048  # images per forward_split call (at least)
+    SPLIT_MIN_BATCH = 10000  # images per forward_split call (at least; ~10 GB of activations)
 
     def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True,
                  deterministic=True, conv="dls"):
@@ -186,8 +186,9 @@ class Inferencer:
         if split is not None:
             # the library's convolutions give every image the same bits whatever
             # batch it runs in (tests/test_gpu_conv.py), so the forward takes at
-            # least SPLIT_MIN_BATCH images at a time: 2000-image batches run a
-            # 10k-image evaluation 4 % faster than 1000 (profiles/r05_conv_probe.txt)
+            # least SPLIT_MIN_BATCH images at a time: a 10k-image evaluation in one
+            # forward runs 3 % faster than in 2,048-image ones and 4 % faster than in
+            # 1,000-image ones (profiles/r05_conv_probe.txt r05bs3)
             bs = max(self.batch_size, self.SPLIT_MIN_BATCH)
             pk = self.model.pack_split()
             for i in range(0, X.shape[0], bs):
