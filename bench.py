@@ -770,7 +770,7 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
                       f"{args.eval_images} CIFAR-10-shaped images (tester batch 1000, forward "
-                      f"batches of {tester.SPLIT_MIN_BATCH}): the library's deterministic convolutions (bf16x3 MFMA, "
+                      f"batches of {server.tester.SPLIT_MIN_BATCH}): the library's deterministic convolutions (bf16x3 MFMA, "
                       f"fused eval batch norm)",
             **rate(el),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
