@@ -762,6 +762,7 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     server.tester.conv, server.tester.fused_eval, server.tester.deterministic = "dls", True, True
     n = len(coal) - 2 * world
     rf = conv_eval_roofline(server.tester) if rank == 0 else None
+    split_batch = server.tester.SPLIT_MIN_BATCH
     del server
     torch.cuda.empty_cache()
     bn = bench_bn_act(args, dev) if rank == 0 else None
@@ -770,7 +771,7 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
                       f"{args.eval_images} CIFAR-10-shaped images (tester batch 1000, forward "
-                      f"batches of {server.tester.SPLIT_MIN_BATCH}): the library's deterministic convolutions (bf16x3 MFMA, "
+                      f"batches of {split_batch}): the library's deterministic convolutions (bf16x3 MFMA, "
                       f"fused eval batch norm)",
             **rate(el),
             "utility_range": [round(min(vals), 4), round(max(vals), 4)],
