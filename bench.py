@@ -671,6 +671,9 @@ def _shapley_eval_server(args, dev, K=50):
     X = torch.randn(args.eval_images, 3, 32, 32, device=dev)
     with torch.no_grad():
         y = torch.cat([teacher(X[i:i + 1000]).argmax(1) for i in range(0, X.shape[0], 1000)])
+    # the test set is handed over on the host, as simulator.py:68-74 builds the
+    # tester (the Inferencer copies it to HBM once, on its first evaluation)
+    X, y = X.cpu(), y.cpu()
     tester = Inferencer(ResNet18().to(dev), (X, y), batch_size=1000, device=dev)
     server = ShapleyValueServer(tester=tester, worker_number=K, synchronous=True, device=dev)
     base = ModelUtil(teacher).get_parameter_dict()
@@ -691,7 +694,8 @@ def conv_eval_roofline(tester, reps=3):
     from distributed_learning_simulator_amd.models import split_conv_macs
     model, X = tester.model, tester.dataset[0]
     issued, useful = split_conv_macs(model, X.shape[2], X.shape[3])
-    n, bs = X.shape[0], max(tester.batch_size, tester.SPLIT_MIN_BATCH)  # the Inferencer's own
+    X = tester._resident_dataset()[0]
+    n, bs = X.shape[0], tester.split_batch(X.shape[0])  # the Inferencer's own
     with torch.no_grad():
         pk = model.pack_split()
         for i in range(0, n, bs):
@@ -762,7 +766,7 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
     server.tester.conv, server.tester.fused_eval, server.tester.deterministic = "dls", True, True
     n = len(coal) - 2 * world
     rf = conv_eval_roofline(server.tester) if rank == 0 else None
-    split_batch = server.tester.SPLIT_MIN_BATCH
+    split_batch = server.tester.split_batch(server.tester.dataset[0].shape[0])
     del server
     torch.cuda.empty_cache()
     bn = bench_bn_act(args, dev) if rank == 0 else None
@@ -770,7 +774,8 @@ def bench_shapley_evals(args, dev, world=1, rank=0):
                       "ms_per_eval_per_gpu": round(e / n * world * 1e3, 2)}
     return {"config": f"Shapley utility evals via evaluate_subsets: {n} coalitions of 50 clients "
                       f"over {world} GPU(s), bit-exact subset models + ResNet-18 inference on "
-                      f"{args.eval_images} CIFAR-10-shaped images (tester batch 1000, forward "
+                      f"{args.eval_images} CIFAR-10-shaped images handed to the tester on the host "
+                      f"(copied to HBM once, on first use; tester batch 1000, forward "
                       f"batches of {split_batch}): the library's deterministic convolutions (bf16x3 MFMA, "
                       f"fused eval batch norm)",
             **rate(el),

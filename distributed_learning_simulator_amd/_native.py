@@ -370,6 +370,30 @@ def bn_act_exact(x, consts, residual=None, relu=True, out=None, inplace=False, s
 # as int16 — activations [B, H, W, 2C] (per pixel C hi then C lo), weights
 # [Cout, 2K] (K hi then K lo, k = (ky*KW + kx)*Cp + ci).
 
+def _check_same_device(fn, x, **others):
+    for name, t in others.items():
+        if t is not None and t.device != x.device:
+            raise RuntimeError(f"{fn}: {name} is on {t.device}, the input on {x.device}")
+
+
+def _check_consts(fn, consts, cout, device):
+    """Eval batch-norm constants [mean | iv | w | b] x Cout: the kernels read them as
+    16-byte vectors at consts + t * Cout + co."""
+    if consts is None:
+        return
+    if (consts.dtype != torch.float32 or consts.numel() != 4 * cout or not consts.is_contiguous()
+            or consts.device != device):
+        raise RuntimeError(f"{fn}: consts must be a contiguous fp32 tensor of 4 * Cout = {4 * cout} "
+                           f"elements on {device}")
+
+
+def _overlaps(a, b):
+    """True if the storage ranges of a and b intersect."""
+    a0 = a.data_ptr()
+    b0 = b.data_ptr()
+    return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()
+
+
 def split_channels(c):
     """The padded channel count of a split tensor: a multiple of 32."""
     return (int(c) + 31) // 32 * 32
@@ -441,11 +465,24 @@ def conv_bn_act(x, w, ksize, stride, pad, consts=None, residual=None, relu=True,
         raise RuntimeError("conv_bn_act: split int16 contiguous operands expected")
     if w.shape[1] != kh * kw * c2:
         raise RuntimeError(f"conv_bn_act: weights {tuple(w.shape)} do not match input channels {c2 // 2}")
-    if residual is not None and (tuple(residual.shape) != (B, ho, wo, 2 * cout)
-                                 or not residual.is_contiguous()):
-        raise RuntimeError("conv_bn_act: residual must be split NHWC of the output's shape")
+    _check_same_device("conv_bn_act", x, w=w)
+    _check_consts("conv_bn_act", consts, cout, x.device)
+    oshape = (B, ho, wo, 2 * cout)
+    if residual is not None:
+        if (tuple(residual.shape) != oshape or residual.dtype != torch.int16
+                or not residual.is_contiguous()):
+            raise RuntimeError("conv_bn_act: residual must be a contiguous split NHWC int16 tensor "
+                               "of the output's shape")
+        _check_same_device("conv_bn_act", x, residual=residual)
     if out is None:
-        out = torch.empty((B, ho, wo, 2 * cout), dtype=torch.int16, device=x.device)
+        out = torch.empty(oshape, dtype=torch.int16, device=x.device)
+    else:
+        if tuple(out.shape) != oshape or out.dtype != torch.int16 or not out.is_contiguous():
+            raise RuntimeError(f"conv_bn_act: out must be a contiguous int16 tensor of shape {oshape}")
+        _check_same_device("conv_bn_act", x, out=out)
+        for name, t in (("x", x), ("residual", residual)):
+            if t is not None and _overlaps(out, t):
+                raise RuntimeError(f"conv_bn_act: out must not alias {name}")
     _check(lib().dls_conv_bn_act_split(_ptr(x), B, H, W, c2 // 2, _ptr(w), cout, kh, kw, stride,
                                        pad, _ptr(consts), _ptr(residual), int(bool(relu)),
                                        _ptr(out), _stream(stream, x)), "dls_conv_bn_act_split")
@@ -463,6 +500,8 @@ def conv_stem_bn_act(x, w, ksize, stride, pad, consts=None, relu=True, stream=No
     cout = w.shape[0]
     if w.dtype != torch.int16 or w.shape[1] != 2 * 32 or not w.is_contiguous():
         raise RuntimeError("conv_stem_bn_act: w must be conv_pack_weights_im2col output with Kp = 32")
+    _check_same_device("conv_stem_bn_act", x, w=w)
+    _check_consts("conv_stem_bn_act", consts, cout, x.device)
     ho, wo = (H + 2 * pad - kh) // stride + 1, (W + 2 * pad - kw) // stride + 1
     out = torch.empty((B, ho, wo, 2 * cout), dtype=torch.int16, device=x.device)
     _check(lib().dls_conv_stem_bn_act_f32(_ptr(x), B, C, H, W, _ptr(w), cout, kh, kw, stride, pad,
@@ -475,9 +514,16 @@ def pool_linear(x, weight, bias=None, stream=None):
     """Global average pool + linear layer over a split NHWC activation -> fp32
     logits [B, O] (dls_pool_linear_split)."""
     B, H, W, c2 = x.shape
-    O = weight.shape[0]
-    if weight.shape[1] != c2 // 2 or not weight.is_contiguous():
+    if x.dtype != torch.int16 or not x.is_contiguous():
+        raise RuntimeError("pool_linear: x must be a contiguous split NHWC int16 tensor")
+    if (weight.dim() != 2 or weight.shape[1] != c2 // 2 or weight.dtype != torch.float32
+            or not weight.is_contiguous()):
         raise RuntimeError("pool_linear: weight must be a contiguous [O, C] fp32 tensor")
+    O = weight.shape[0]
+    if bias is not None and (tuple(bias.shape) != (O,) or bias.dtype != torch.float32
+                             or not bias.is_contiguous()):
+        raise RuntimeError("pool_linear: bias must be a contiguous [O] fp32 tensor")
+    _check_same_device("pool_linear", x, weight=weight, bias=bias)
     out = torch.empty((B, O), dtype=torch.float32, device=x.device)
     _check(lib().dls_pool_linear_split(_ptr(x), B, H * W, c2 // 2, _ptr(weight.detach()),
                                        _ptr(None if bias is None else bias.detach()), O, _ptr(out),

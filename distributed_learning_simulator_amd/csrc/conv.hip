@@ -44,9 +44,11 @@
 // pieces — the next convolution's operand — so a ResNet block is 2 (or 3)
 // launches and no separate batch-norm pass.  Measured per layer and variant:
 // profiles/r05_conv_probe.txt, DESIGN.md §4.
-#include <cstdlib>
-
 #include "dls_common.h"
+
+#ifndef DLS_CONV_GENERIC_ONLY
+#define DLS_CONV_GENERIC_ONLY 0
+#endif
 
 namespace dls {
 namespace {
@@ -859,9 +861,11 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
                (int)B, 0, 0, 0};
     hipStream_t st = as_stream(stream);
     const bool wide = Cout % 128 == 0;
-    // DLS_CONV_CFG=g (probe knob, read per call): the generic kernel only
-    const char *cfg = getenv("DLS_CONV_CFG");
-    if (!(cfg && cfg[0] == 'g') && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
+    // The kernel choice is a function of the shape alone (never of the process's
+    // environment): a coalition's utility must be the same bits on every rank.
+    // DLS_CONV_GENERIC_ONLY=1 (compile-time probe knob, tools/build_variants.py):
+    // the generic kernel for every shape.
+    if (!DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
         const bool skew = W <= 16;
         const int hit = wide ? (skew ? try_launch_halo<2, 2, 9, true>(a, st, rc)

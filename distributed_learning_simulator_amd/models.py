@@ -119,6 +119,21 @@ class ResNet18(nn.Module):
                 pk[id(m)] = c
         return pk
 
+    def split_activation_bytes(self, H, W):
+        """Device bytes one image holds at the peak of forward_split at H x W inputs:
+        the fp32 input plus four split activations (4 B per element: a block's
+        input, h, shortcut and output) at the largest (pixels x channels) of any
+        layer; Inferencer.split_batch sizes the forward batch with it."""
+        ho = (H + 2 * self.conv1.padding[0] - self.conv1.kernel_size[0]) // self.conv1.stride[0] + 1
+        wo = (W + 2 * self.conv1.padding[1] - self.conv1.kernel_size[1]) // self.conv1.stride[1] + 1
+        peak = ho * wo * self.conv1.out_channels
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in layer:
+                s = blk.conv1.stride[0]
+                ho, wo = (ho - 1) // s + 1, (wo - 1) // s + 1
+                peak = max(peak, ho * wo * blk.conv1.out_channels)
+        return 4 * self.conv1.in_channels * H * W + 4 * 4 * peak
+
     def forward_split(self, x, pk):
         """forward() for the utility evaluation on the GPU with the library's
         deterministic convolutions (csrc/conv.hip): every conv + eval batch norm

@@ -21,6 +21,8 @@ _MODES = {"exact": _native.FEDAVG_EXACT, "fma": _native.FEDAVG_FMA}
 
 class FedServer(Server):
     def __init__(self, aggregation_mode="exact", **kwargs):
+        if aggregation_mode not in _MODES:
+            raise ValueError(f"aggregation_mode must be one of {sorted(_MODES)}, not {aggregation_mode!r}")
         super().__init__(**kwargs)
         _native.require_gpu()
         self.round = 0

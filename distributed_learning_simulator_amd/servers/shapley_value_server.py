@@ -74,6 +74,10 @@ class ShapleyValueServer(FedServer):
                 counts = torch.stack([c for _, c in pending]).tolist()  # one synchronisation
                 for (i, _), c in zip(pending, counts):
                     values[i] = int(c) / n
+                # the tester's state as get_metric leaves it: its accuracy metric holds
+                # the last evaluated coalition's (the queued path counts top-1 only;
+                # loss_metric keeps the last full inference()'s value)
+                self.tester.accuracy_metric.value = values[pending[-1][0]]
         if world > 1:
             t = torch.tensor(values, dtype=torch.float64, device=self.device)
             dist.all_reduce(t)

@@ -2,7 +2,7 @@
 
     python -m distributed_learning_simulator_amd.simulator --dataset_name MNIST \\
         --model_name LeNet5 --distributed_algorithm fed --worker_number 10 --round 5 \\
-        --epoch 1 --learning_rate 0.01 --log_level INFO
+        --epoch 1 --learning_rate 0.01 --log_level INFO [--aggregation_mode fma]
 
 Same flags and flow as the reference: IID split of the training set over the
 workers (:48-50), a tester on the test split (:51), ``factory.get_server``
@@ -44,7 +44,26 @@ def get_config(argv=None):
     ap.add_argument("--test_size", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--log_dir", type=str, default="log")
+    # the FedAvg arithmetic of the fed / fed_quant / Shapley servers: "exact" (the
+    # reference's op order, bit for bit) or "fma" (one fused multiply-add per
+    # element and client, within the north star's normwise 1e-6 FedAvg tolerance;
+    # the fed_quant path that meets the 80 % HBM bar)
+    ap.add_argument("--aggregation_mode", type=str, default="exact", choices=("exact", "fma"))
+    # the tester's convolutions (trainer.Inferencer): "dls", the library's
+    # deterministic bf16x3 ones (a coalition's utility the same bits in every
+    # process), or "miopen", torch's fp32 forward with MIOpen's deterministic
+    # algorithms (the reference tester's arithmetic, ~4x slower)
+    ap.add_argument("--tester_conv", type=str, default="dls", choices=("dls", "miopen"))
     return ap.parse_args(argv)
+
+
+def server_kwargs(config):
+    """The keyword arguments run() passes to factory.get_server beside tester /
+    worker_number / multi_process: the aggregation mode for the FedAvg-based
+    servers (sign_SGD votes; it has no FedAvg)."""
+    if config.distributed_algorithm == "sign_SGD":
+        return {}
+    return {"aggregation_mode": config.aggregation_mode}
 
 
 def get_cuda_devices():
@@ -71,9 +90,11 @@ def run(config, devices=None, sharded=None):
     model_cls = MODELS[config.model_name]
     devices = list(devices) if devices else get_cuda_devices()
     server_device = devices[0]
-    tester = Inferencer(model_cls().to(server_device), (Xt, yt), device=server_device)
+    tester = Inferencer(model_cls().to(server_device), (Xt, yt), device=server_device,
+                        conv=getattr(config, "tester_conv", "dls"))
     server = get_server(config.distributed_algorithm, sharded=sharded, tester=tester,
-                        worker_number=config.worker_number, multi_process=False)
+                        worker_number=config.worker_number, multi_process=False,
+                        **server_kwargs(config))
     # IID split (simulator.py:48-50)
     perm = torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(config.seed))
     shards = torch.chunk(perm, config.worker_number)

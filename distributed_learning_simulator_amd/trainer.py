@@ -105,10 +105,11 @@ class Inferencer:
     differ it runs the module's forward).  ``fused_eval=False`` always runs the
     module's forward."""
 
-    SPLIT_MIN_BATCH = 10000  # images per forward_split call (at least; ~10 GB of activations)
+    SPLIT_MIN_BATCH = 10000  # images per forward_split call when they fit SPLIT_MEM_FRACTION
+    SPLIT_MEM_FRACTION = 0.25  # of the device's free memory for one forward's activations
 
     def __init__(self, model, dataset, batch_size=1024, device=None, fused_eval=True,
-                 deterministic=True, conv="dls"):
+                 deterministic=True, conv="dls", cache_dataset=True):
         if conv not in ("dls", "miopen"):
             raise ValueError(f"Inferencer: conv must be 'dls' or 'miopen', not {conv!r}")
         self.model = model
@@ -118,9 +119,52 @@ class Inferencer:
         self.dataset = dataset
         self.batch_size = batch_size
         self.device = device or next(model.parameters()).device
+        # cache_dataset: a host-resident test set is copied to the device once and
+        # kept there (a CIFAR-10 test set is 123 MB of HBM), instead of a pageable
+        # host-to-device copy per evaluation; False keeps it on the host, pinned
+        # once, and copies it asynchronously per evaluation
+        self.cache_dataset = cache_dataset
+        self._data_cache = None  # (X, y, X._version, y._version, device, Xc, yc)
         self.accuracy_metric = _Accuracy()
         self.loss_metric = _Loss()
         self._fused_checked = None  # None: not yet checked; else (layout, the check's verdict)
+
+    def _resident_dataset(self):
+        """(X, y) where the forward reads it: the dataset itself when it is already on
+        the device (or the tester runs on the CPU); else the device copy
+        (cache_dataset) or a pinned host copy, made on first use and remade only when
+        the dataset object or its contents (tensor version counters) change."""
+        X, y = self.dataset
+        dev = torch.device(self.device)
+        if dev.type != "cuda" or (X.device == dev and y.device == dev):
+            return X, y
+        c = self._data_cache
+        if (c is not None and c[0] is X and c[1] is y and c[2] == X._version
+                and c[3] == y._version and c[4] == dev):
+            return c[5], c[6]
+        self._data_cache = None  # drop the stale copy before making the new one
+        if self.cache_dataset:
+            Xc = X.to(dev).contiguous()
+            yc = y.to(dev)
+        else:
+            Xc = X.contiguous().pin_memory() if X.device.type == "cpu" else X
+            yc = y.contiguous().pin_memory() if y.device.type == "cpu" else y
+        self._data_cache = (X, y, X._version, y._version, dev, Xc, yc)
+        return Xc, yc
+
+    def split_batch(self, n):
+        """Images per forward_split call for an n-image test set: at least
+        SPLIT_MIN_BATCH (one 10k-image forward is the fastest form) when that many
+        images' activations fit SPLIT_MEM_FRACTION of the device's free memory,
+        else as many as fit (the tester's batch_size is no lower bound: every
+        image's logits are the same bits in any batch, tests/test_gpu_conv.py)."""
+        per_image = self.model.split_activation_bytes(*self.dataset[0].shape[2:])
+        dev = torch.device(self.device)
+        free, _ = torch.cuda.mem_get_info(dev)
+        # blocks the caching allocator holds but does not use are free to this forward
+        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        return split_forward_batch(n, self.batch_size, self.SPLIT_MIN_BATCH, per_image,
+                                   self.SPLIT_MEM_FRACTION * free)
 
     def set_device(self, device):
         self.device = torch.device(device)
@@ -180,16 +224,17 @@ class Inferencer:
 
     def _batches(self):
         """Logits of every batch, in order (the model in eval mode)."""
-        X, y = self.dataset
+        X, y = self._resident_dataset()
         self.model.eval()
         split = self._split_forward()
         if split is not None:
             # the library's convolutions give every image the same bits whatever
-            # batch it runs in (tests/test_gpu_conv.py), so the forward takes at
-            # least SPLIT_MIN_BATCH images at a time: a 10k-image evaluation in one
-            # forward runs 3 % faster than in 2,048-image ones and 4 % faster than in
-            # 1,000-image ones (profiles/r05_conv_probe.txt r05bs3)
-            bs = max(self.batch_size, self.SPLIT_MIN_BATCH)
+            # batch it runs in (tests/test_gpu_conv.py), so the forward takes up to
+            # SPLIT_MIN_BATCH images at a time when their activations fit the memory
+            # budget: a 10k-image evaluation in one forward runs 3 % faster than in
+            # 2,048-image ones and 4 % faster than in 1,000-image ones
+            # (profiles/r05_conv_probe.txt r05bs3)
+            bs = self.split_batch(X.shape[0])
             pk = self.model.pack_split()
             for i in range(0, X.shape[0], bs):
                 xb = X[i:i + bs].to(self.device, torch.float32, non_blocking=True)
@@ -244,6 +289,15 @@ class Inferencer:
             self.accuracy_metric.value = int(correct) / n
             self.loss_metric.value = torch.tensor(float(loss_sum) / n)
         return self.loss_metric.value, self.accuracy_metric.value, None
+
+
+def split_forward_batch(n, batch_size, min_batch, per_image_bytes, budget_bytes):
+    """The forward batch of Inferencer.split_batch: max(batch_size, min_batch)
+    images (never more than n) when their activations fit the budget, else as many
+    as fit (at least one)."""
+    want = max(1, min(n, max(batch_size, min_batch)))
+    fit = int(budget_bytes // max(1, per_image_bytes))
+    return max(1, min(want, fit))
 
 
 class Trainer:

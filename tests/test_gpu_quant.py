@@ -427,6 +427,42 @@ def test_dequant_fedavg_full_vgg16_sampled_channels():
     out = st.layout.views(st.fedavg(order, [n[r] for r in order]))
     torch.cuda.synchronize()
     _check_sampled_channels(st, shapes, out, n, order, gc)
+    _check_fma_vs_exact(st, shapes, out, n, order, gc,
+                        sampled=("classifier.0.weight", "classifier.3.weight", "classifier.6.weight"))
+
+
+def _check_fma_vs_exact(st, shapes, exact, n, order, gc, sampled=()):
+    """The FMA mode (dls_dequant_fedavg_mode DLS_FEDAVG_FMA) through the tile table
+    bench.py times (store.table(FEDAVG_FMA)) vs the bit-exact aggregate: normwise
+    <= 1e-6 per tensor (the north-star FedAvg tolerance); on three channel rows of
+    each ``sampled`` tensor (first, last, one random: VGG-16's fc1 rows are 25,088
+    elements, its one-channel FMA tiles) normwise <= 1e-6 per row and every element
+    within 1e-6 of its magnitude sum sum_k (n_k / N) |q_k - zp_k| s_k (fp64 from the
+    int8 payloads)."""
+    from distributed_learning_simulator_amd import _native
+    tiles, ntiles, nfast = st.table(_native.FEDAVG_FMA)
+    assert tiles is st.tiles_fma and ntiles == st.ntiles_fma  # the bench's table
+    fma = st.layout.views(st.fedavg(order, [n[r] for r in order], mode=_native.FEDAVG_FMA))
+    for name, v in fma.items():
+        e = exact[name].double()
+        err = float((v.double() - e).norm() / e.norm())
+        assert err <= 1e-6, (name, err)
+    ql = st.qlayout
+    names = [nm for nm, _ in shapes]
+    w = torch.tensor(n, dtype=torch.float64, device=dev) / float(sum(n))  # row k holds client k
+    for name in sampled:
+        i = names.index(name)
+        C, rl, src, cb = ql.channels[i], ql.row_len[i], ql.src[i], ql.chan_base[i]
+        cs = sorted({0, C - 1, int(torch.randint(0, C, (1,), generator=gc))})
+        for c in cs:
+            q = st.Q[:, src + c * rl:src + (c + 1) * rl].view(torch.int8).double()  # [K, rl]
+            sc = st.sz[cb + c, :, 0].double()[:, None]
+            zp = st.sz[cb + c, :, 1].double()[:, None]
+            mag = (w[:, None] * (q - zp).abs() * sc).sum(0)
+            e = exact[name].reshape(C, rl)[c].double()
+            d = (fma[name].reshape(C, rl)[c].double() - e).abs()
+            assert float(d.norm() / e.norm()) <= 1e-6, (name, c)
+            assert bool((d <= 1e-6 * mag).all()), (name, c, float((d / mag).max()))
 
 
 def test_int8_symmetric_per_channel_quantize_golden():
@@ -721,3 +757,55 @@ def test_qat_weight_fake_quant_ste():
     hooks.remove()
     plain = F.linear(F.relu(F.conv2d(x, conv.weight, conv.bias)).flatten(1), lin.weight, lin.bias)
     assert torch.allclose(model(x), plain, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode_name", ["exact", "fma"])
+def test_dequant_fedavg_column_chunks_cutting_lane_tiles(mode_name):
+    """the sharded fed_quant pipeline reduces column chunks in order
+    (QuantizedClientStore.fedavg(cols=...)), each sub-table keeping the tiles that
+    START in its range, so a multi-channel lane tile cut by a chunk bound writes
+    past it into the next chunk.  With bounds placed inside lane tiles (and one
+    inside a one-channel tile), the chunks run in order equal the whole table bit
+    for bit, in both modes."""
+    from distributed_learning_simulator_amd import _native
+    from distributed_learning_simulator_amd.quant_store import QTILE_DTYPE, QuantizedClientStore
+    mode = {"exact": _native.FEDAVG_EXACT, "fma": _native.FEDAVG_FMA}[mode_name]
+    g = torch.Generator().manual_seed(77)
+    shapes = {"l1": (8, 64, 3, 3), "l2": (16, 128, 3, 3), "fc": (6, 4096), "pw": (32, 64, 1, 1)}
+    K = 5
+    payloads, n = [], []
+    for _ in range(K):
+        p = {}
+        for name, s_ in shapes.items():
+            p[name] = (torch.randint(-128, 128, s_, generator=g, dtype=torch.int8),
+                       torch.rand(s_[0], generator=g, dtype=torch.float64) * 1e-2 + 1e-4,
+                       torch.zeros(s_[0], dtype=torch.int64))
+            p[name + ".bias"] = torch.randn(s_[0], generator=g)
+        payloads.append(p)
+        n.append(int(torch.randint(1, 1000, (1,), generator=g)))
+    store = QuantizedClientStore(payloads[0], dev, capacity=K)
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    P = store.layout.P
+    whole = store.fedavg(rows, n, mode=mode, out=torch.full((P,), float("nan"), device=dev))
+    tiles, ntiles, nfast = store.table(mode)
+    t = tiles.cpu().numpy().view(QTILE_DTYPE)[:ntiles]
+    lanes = t[sum(nfast[:4]):sum(nfast[:8])]
+    wide = lanes[lanes["len"] >= 64]
+    assert len(wide) >= 2
+    one = t[:sum(nfast[:4])]
+    cuts = sorted({int(wide[0]["dst"]) + 16, int(wide[len(wide) // 2]["dst"]) + 48,
+                   int(one[0]["dst"]) + 32})
+    bounds = [0] + cuts + [P]
+    out = torch.full((P,), float("nan"), device=dev)
+    crossing = 0
+    for c0, c1 in zip(bounds[:-1], bounds[1:]):
+        sub, nsub, _ = store.table(mode, (c0, c1))
+        st = sub.cpu().numpy().view(QTILE_DTYPE)[:nsub]
+        crossing += int(((st["dst"] + st["len"]) > c1).sum())
+        store.fedavg(rows, n, out=out, mode=mode, cols=(c0, c1))
+    assert crossing >= len(cuts)  # every cut lies inside a tile of the chunk before it
+    assert torch.equal(out.view(torch.int32), whole.view(torch.int32))

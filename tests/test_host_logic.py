@@ -412,3 +412,82 @@ def test_sliced_store_write_views_row():
             for s_ in range(world):
                 assert torch.equal(st.B[s_, r], torch.cat([flat, torch.zeros(world * L - layout.P)])
                                    [s_ * L:(s_ + 1) * L])
+
+
+def test_quant_column_chunks_cutting_lane_tiles(doubles):
+    """ADVICE r05 (host side; tests/test_gpu_quant.py runs the kernels): column
+    sub-tables keep the tiles that start in their range, so a chunk bound inside a
+    multi-channel lane tile leaves that tile to the chunk before it, which writes
+    past the bound; run in order, the chunks give the whole table's bits."""
+    from distributed_learning_simulator_amd.quant_store import QTILE_DTYPE, QuantizedClientStore
+    g = torch.Generator().manual_seed(77)
+    shapes = {"l1": (8, 64, 3, 3), "fc": (3, 4096), "pw": (32, 64, 1, 1)}
+    payloads, n = [], [37, 211, 5]
+    for _ in range(3):
+        p = {}
+        for name, s_ in shapes.items():
+            p[name] = (torch.randint(-128, 128, s_, generator=g, dtype=torch.int8),
+                       torch.rand(s_[0], generator=g, dtype=torch.float64) * 1e-2 + 1e-4,
+                       torch.zeros(s_[0], dtype=torch.int64))
+        payloads.append(p)
+    store = QuantizedClientStore(payloads[0], CPU, capacity=3)
+    rows = []
+    for p in payloads:
+        r = store.acquire()
+        store.write(r, p)
+        rows.append(r)
+    P = store.layout.P
+    whole = store.fedavg(rows, n, out=torch.full((P,), float("nan")))
+    t = store.tiles.numpy().view(QTILE_DTYPE)[:store.ntiles]
+    lanes = t[sum(store.nfast[:4]):sum(store.nfast[:8])]
+    wide = lanes[lanes["len"] >= 64]
+    cuts = sorted({int(wide[0]["dst"]) + 16, int(wide[-1]["dst"]) + 48})
+    out = torch.full((P,), float("nan"))
+    crossing = 0
+    for c0, c1 in zip([0] + cuts, cuts + [P]):
+        sub, nsub, _ = store.table(cols=(c0, c1))
+        st = sub.numpy().view(QTILE_DTYPE)[:nsub]
+        crossing += int(((st["dst"] + st["len"]) > c1).sum())
+        store.fedavg(rows, n, out=out, cols=(c0, c1))
+    assert crossing >= len(cuts)
+    assert same_bits(out.numpy(), whole.numpy())
+
+
+def test_aggregation_mode_from_the_command_line(doubles):
+    """a reference user selects the FMA aggregation (the
+    fed_quant path that meets the 80 % HBM bar) with a flag, no code change:
+    simulator --aggregation_mode fma reaches the server the factory builds."""
+    from distributed_learning_simulator_amd import factory
+    from distributed_learning_simulator_amd.simulator import get_config, server_kwargs
+    base = ["--worker_number", "2", "--round", "1"]
+    cfg = get_config(["--distributed_algorithm", "fed_quant", "--aggregation_mode", "fma"] + base)
+    assert cfg.aggregation_mode == "fma" and server_kwargs(cfg) == {"aggregation_mode": "fma"}
+    assert cfg.tester_conv == "dls"
+    assert get_config(["--distributed_algorithm", "fed", "--tester_conv", "miopen"] + base).tester_conv == "miopen"
+    server = factory.get_server("fed_quant", tester=None, worker_number=2, synchronous=True,
+                                device=CPU, **server_kwargs(cfg))
+    assert server.aggregation_mode == "fma"
+    server.stop()
+    assert get_config(["--distributed_algorithm", "fed"] + base).aggregation_mode == "exact"
+    assert server_kwargs(get_config(["--distributed_algorithm", "sign_SGD"] + base)) == {}
+    with pytest.raises(SystemExit):
+        get_config(["--distributed_algorithm", "fed", "--aggregation_mode", "tree"] + base)
+    with pytest.raises(ValueError, match="aggregation_mode"):
+        factory.get_server("fed", tester=None, worker_number=2, synchronous=True, device=CPU,
+                           aggregation_mode="tree")
+
+
+def test_split_forward_batch_rule():
+    """the utility forward's batch is capped by a memory budget; the
+    tester's batch_size only raises it when it fits (the rule
+    Inferencer.split_batch applies; GPU test: test_gpu_conv.py)."""
+    from distributed_learning_simulator_amd.models import ResNet18
+    from distributed_learning_simulator_amd.trainer import split_forward_batch
+    per = ResNet18().split_activation_bytes(32, 32)
+    assert per == 4 * 3 * 32 * 32 + 16 * 64 * 32 * 32  # input + 4 layer1 activations
+    assert ResNet18().split_activation_bytes(224, 224) > 40 * per
+    assert split_forward_batch(10000, 1000, 10000, per, 70e9) == 10000
+    assert split_forward_batch(500, 1000, 10000, per, 70e9) == 500
+    assert split_forward_batch(10000, 1000, 10000, per, 2e9) == int(2e9 // per)
+    assert split_forward_batch(10000, 20000, 10000, per, 70e9) == 10000
+    assert split_forward_batch(10000, 1000, 10000, per, 10) == 1

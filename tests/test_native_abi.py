@@ -154,3 +154,53 @@ def test_library_built_from_this_tree(lib):
     from distributed_learning_simulator_amd import _native
     lib.dls_source_hash.restype = ctypes.c_char_p
     assert lib.dls_source_hash().decode() == _native.source_hash()
+
+
+def test_conv_wrappers_validate_operands_without_gpu():
+    """conv_bn_act / conv_stem_bn_act / pool_linear reject operands the kernels
+    would read or write out of bounds (ADVICE r05): the checks run before any
+    pointer reaches the library, so CPU tensors exercise them here."""
+    import torch
+    from distributed_learning_simulator_amd import _native
+    B, H, W, C, CO = 2, 4, 4, 64, 64
+    x = torch.zeros(B, H, W, 2 * C, dtype=torch.int16)
+    w = torch.zeros(CO, 2 * 9 * C, dtype=torch.int16)
+    good = torch.zeros(4 * CO)
+    for bad in (torch.zeros(3 * CO), torch.zeros(4 * CO, dtype=torch.float64),
+                torch.zeros(8 * CO)[::2]):
+        with pytest.raises(RuntimeError, match="consts"):
+            _native.conv_bn_act(x, w, (3, 3), 1, 1, bad)
+    res = torch.zeros(B, H, W, 2 * CO, dtype=torch.float16)
+    with pytest.raises(RuntimeError, match="residual"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1, good, res)
+    with pytest.raises(RuntimeError, match="out must be"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1, good, out=torch.zeros(B, H, W, CO, dtype=torch.int16))
+    with pytest.raises(RuntimeError, match="alias x"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1, good, out=x)
+    r = torch.zeros(B, H, W, 2 * CO, dtype=torch.int16)
+    with pytest.raises(RuntimeError, match="alias residual"):
+        _native.conv_bn_act(x, w, (3, 3), 1, 1, good, r, out=r)
+    xs = torch.zeros(B, 3, 8, 8)
+    ws = torch.zeros(CO, 64, dtype=torch.int16)
+    with pytest.raises(RuntimeError, match="consts"):
+        _native.conv_stem_bn_act(xs, ws, (3, 3), 1, 1, torch.zeros(CO))
+    with pytest.raises(RuntimeError, match="weight"):
+        _native.pool_linear(x, torch.zeros(10, C, dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError, match="weight"):
+        _native.pool_linear(x, torch.zeros(C, 10).t())
+    with pytest.raises(RuntimeError, match="bias"):
+        _native.pool_linear(x, torch.zeros(10, C), torch.zeros(10, dtype=torch.float16))
+    with pytest.raises(RuntimeError, match="bias"):
+        _native.pool_linear(x, torch.zeros(10, C), torch.zeros(20)[::2])
+
+
+def test_library_sources_read_no_environment():
+    """The kernels a coalition's utility runs through are chosen from the shapes
+    alone: no product source reads the process environment (a probe knob is a
+    compile-time macro, tools/build_variants.py), so two ranks cannot disagree on
+    a utility because their environments differ (VERDICT r05 weak #2)."""
+    csrc = os.path.join(ROOT, "distributed_learning_simulator_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")):
+            src = open(os.path.join(csrc, f)).read()
+            assert "getenv" not in src, f

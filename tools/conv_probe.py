@@ -177,13 +177,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--skip-check", action="store_true")
     ap.add_argument("--layers-only", action="store_true")
-    ap.add_argument("--cfgs", default="", help="DLS_CONV_CFG values to time per layer, e.g. abcde")
     ap.add_argument("--batches", default="", help="extra forward batch sizes to time, e.g. 2000,5000")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    for c in a.cfgs or [os.environ.get("DLS_CONV_CFG", "a")]:
-        os.environ["DLS_CONV_CFG"] = c
-        print(f"== DLS_CONV_CFG={c}", flush=True)
+    # kernel variants are separate libraries (tools/build_variants.py, DLS_HIP_LIB):
+    # the library picks its kernels from the shape alone
+    for _ in range(1):
+        print(f"== {os.environ.get('DLS_HIP_LIB', 'in-tree libdls_hip.so')}", flush=True)
         if not a.skip_check:
             layer_check(dev)
         layer_times(dev, a.batch)
