@@ -257,12 +257,28 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
     }
 }
 
-// XCD-aware tile order: the 8 XCDs take consecutive blockIdx round-robin; give
-// each a contiguous run of (pixel tile, channel tile) pairs, channel tile fastest,
-// so blocks reading the same input pixels share an L2
-__device__ __forceinline__ int tile_of_block() {
-    const int nblk = gridDim.x, bid = blockIdx.x;
-    return (nblk & 7) == 0 ? (bid & 7) * (nblk >> 3) + (bid >> 3) : bid;
+// XCD-aware tile order: the 8 XCDs take consecutive blockIdx round-robin (block
+// b on XCD b % 8); give each XCD a contiguous run of tiles (any grid size: XCD x
+// holds ceil((nblk - x) / 8) blocks).  Default order: (pixel tile, channel tile)
+// pairs, channel tile fastest, so blocks reading the same input pixels share an
+// L2.  DLS_CONV_XCD_COMAJOR=1 (probe knob): channel tile slowest, so an XCD's
+// blocks share its channel tiles' weights instead.
+#ifndef DLS_CONV_XCD_COMAJOR
+#define DLS_CONV_XCD_COMAJOR 0
+#endif
+__device__ __forceinline__ void tile_of_block(int co_tiles, int &co_t, int &pix_t) {
+    const int nblk = gridDim.x, bid = blockIdx.x, x = bid & 7;
+    // blocks on XCDs 0..x-1: sum of ceil((nblk - j) / 8)
+    const int q = nblk >> 3, rmd = nblk & 7;
+    const int t = x * q + (x < rmd ? x : rmd) + (bid >> 3);
+    if (DLS_CONV_XCD_COMAJOR) {
+        const int pix_tiles = nblk / co_tiles;
+        co_t = t / pix_tiles;
+        pix_t = t - co_t * pix_tiles;
+    } else {
+        co_t = t % co_tiles;
+        pix_t = t / co_tiles;
+    }
 }
 
 // ---------------------------------------------------------------- generic
@@ -291,9 +307,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
-    const int t = tile_of_block();
-    const int co0 = (t % a.co_tiles) * BMC;
-    const int pix0 = (t / a.co_tiles) * BNP;
+    int co_t, pix_t;
+    tile_of_block(a.co_tiles, co_t, pix_t);
+    const int co0 = co_t * BMC;
+    const int pix0 = pix_t * BNP;
 
     // staging assignment: piece `part` of rows tid / PPR + RPP * u
     const int part = tid % PPR, row0 = tid / PPR;
@@ -421,9 +438,9 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
-    const int t = tile_of_block();
-    const int co0 = (t % a.co_tiles) * BMC;
-    const int pt = t / a.co_tiles;
+    int co_t, pt;
+    tile_of_block(a.co_tiles, co_t, pt);
+    const int co0 = co_t * BMC;
     const int pix0 = pt * BNP;
     const int W = a.W, H = a.H, W2 = W + 2;
     const int hrows_img = (a.TR + 2) * W2;
@@ -554,9 +571,10 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
     uint8_t *Bs = smem;
     const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int t = tile_of_block();
-    const int co0 = (t % a.co_tiles) * kWaveTile;
-    const int pix0 = (t / a.co_tiles) * BNP;
+    int co_t, pix_t;
+    tile_of_block(a.co_tiles, co_t, pix_t);
+    const int co0 = co_t * kWaveTile;
+    const int pix0 = pix_t * BNP;
     // A fragments of both k-steps (in flight during the gather): channel tile i,
     // lane row co0 + 32 i + r, k = 16 s + 8 h .. + 7 (hi), + K (lo)
     Frag f[kBK / 16];

@@ -796,9 +796,11 @@ def test_dequant_fedavg_column_chunks_cutting_lane_tiles(mode_name):
     lanes = t[sum(nfast[:4]):sum(nfast[:8])]
     wide = lanes[lanes["len"] >= 64]
     assert len(wide) >= 2
-    one = t[:sum(nfast[:4])]
-    cuts = sorted({int(wide[0]["dst"]) + 16, int(wide[len(wide) // 2]["dst"]) + 48,
-                   int(one[0]["dst"]) + 32})
+    one = t[:sum(nfast[:4])]  # one-channel tiles (the EXACT table's fc rows; FMA: none)
+    cuts = {int(wide[0]["dst"]) + 16, int(wide[len(wide) // 2]["dst"]) + 48}
+    if len(one):
+        cuts.add(int(one[0]["dst"]) + 32)
+    cuts = sorted(cuts)
     bounds = [0] + cuts + [P]
     out = torch.full((P,), float("nan"), device=dev)
     crossing = 0
