@@ -111,8 +111,12 @@ typedef f32x16 WaveAcc[2][2];
 // (this lane's row r of the wave's first 32-channel tile; the second at +32
 // rows), B rows of the two 32-pixel tiles at b0 / b1 (this lane's pixel).
 // Products in the fixed order lo*hi, hi*lo, hi*hi per k-step.
+#ifndef DLS_CONV_PRIO
+#define DLS_CONV_PRIO 0
+#endif
 __device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, const uint8_t *b0,
                                            const uint8_t *b1, int h) {
+    if (DLS_CONV_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < kBK / 16; ++s) {
         const int off = 32 * s + 16 * h;  // bytes: k = 16 s + 8 h .. + 7
@@ -135,6 +139,7 @@ __device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, co
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
             }
     }
+    if (DLS_CONV_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // One k-step's fragments (16 channels): A hi / lo of the wave's two channel
