@@ -111,25 +111,24 @@ typedef f32x16 WaveAcc[2][2];
 // (this lane's row r of the wave's first 32-channel tile; the second at +32
 // rows), B rows of the two 32-pixel tiles at b0 / b1 (this lane's pixel).
 // Products in the fixed order lo*hi, hi*lo, hi*hi per k-step.
-#ifndef DLS_CONV_PRIO
-#define DLS_CONV_PRIO 0
-#endif
+// BK: channels per chunk (an LDS row holds BK hi, BK lo and a 16-B pad)
+template <int BK = kBK>
 __device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, const uint8_t *b0,
                                            const uint8_t *b1, int h) {
-    if (DLS_CONV_PRIO) __builtin_amdgcn_s_setprio(1);
+    constexpr int RB = 4 * BK + 16;
 #pragma unroll
-    for (int s = 0; s < kBK / 16; ++s) {
+    for (int s = 0; s < BK / 16; ++s) {
         const int off = 32 * s + 16 * h;  // bytes: k = 16 s + 8 h .. + 7
         bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            ah[i] = *reinterpret_cast<const bf16x8 *>(arow + i * 32 * kRowB + off);
-            al[i] = *reinterpret_cast<const bf16x8 *>(arow + i * 32 * kRowB + 2 * kBK + off);
+            ah[i] = *reinterpret_cast<const bf16x8 *>(arow + i * 32 * RB + off);
+            al[i] = *reinterpret_cast<const bf16x8 *>(arow + i * 32 * RB + 2 * BK + off);
         }
         bh[0] = *reinterpret_cast<const bf16x8 *>(b0 + off);
-        bl[0] = *reinterpret_cast<const bf16x8 *>(b0 + 2 * kBK + off);
+        bl[0] = *reinterpret_cast<const bf16x8 *>(b0 + 2 * BK + off);
         bh[1] = *reinterpret_cast<const bf16x8 *>(b1 + off);
-        bl[1] = *reinterpret_cast<const bf16x8 *>(b1 + 2 * kBK + off);
+        bl[1] = *reinterpret_cast<const bf16x8 *>(b1 + 2 * BK + off);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -139,7 +138,6 @@ __device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, co
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
             }
     }
-    if (DLS_CONV_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // One k-step's fragments (16 channels): A hi / lo of the wave's two channel
@@ -192,6 +190,20 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
     const int lc = 8 * (tid % GPP);  // a thread's channel group is fixed per pass
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
+        const int co = co0 + (NPASS == 1 ? lc : (lc / 32) * kWaveTile + 32 * p + lc % 32);
+        // the pass's residual pieces are loaded before the transpose, their
+        // latency behind its LDS writes and barrier (-1 to -2 % on the residual
+        // layers, profiles/r06_conv_ab.txt)
+        u32x4 rpf[NPC][2];
+        if (a.res) {
+#pragma unroll
+            for (int u = 0; u < NPC; ++u) {
+                const int px = pix0 + (tid + NT * u) / GPP;
+                const int64_t ob = (int64_t)(px < a.M ? px : 0) * (2 * a.Cout) + co;
+                rpf[u][0] = *reinterpret_cast<const u32x4 *>(a.res + ob);
+                rpf[u][1] = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
+            }
+        }
         if (p > 0) __syncthreads();  // the previous pass's reads are done
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -207,7 +219,6 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
                 }
             }
         __syncthreads();
-        const int co = co0 + (NPASS == 1 ? lc : (lc / 32) * kWaveTile + 32 * p + lc % 32);
         // the 8 channels' batch-norm constants as element pairs: 8 vector loads
         f32x2 m2[4], iv2[4], wv2[4], bv2[4];
         if (a.consts) {
@@ -227,7 +238,7 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
                 bv2[2 * hh + 1] = f32x2{cb[2], cb[3]};
             }
         }
-#pragma unroll 2
+#pragma unroll
         for (int u = 0; u < NPC; ++u) {
             const int pl = (tid + NT * u) / GPP;
             const int px = pix0 + pl;
@@ -241,8 +252,7 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
                 for (int q = 0; q < 4; ++q) v2[q] = __builtin_elementwise_fma(wv2[q], (v2[q] - m2[q]) * iv2[q], bv2[q]);
             }
             if (a.res) {  // + (hi + lo)
-                const u32x4 rh = *reinterpret_cast<const u32x4 *>(a.res + ob);
-                const u32x4 rl = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
+                const u32x4 rh = rpf[u][0], rl = rpf[u][1];
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     v2[q] = v2[q] + (f32x2{__uint_as_float(rh[q] << 16), __uint_as_float(rh[q] & 0xffff0000u)} +
@@ -264,26 +274,17 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
 
 // XCD-aware tile order: the 8 XCDs take consecutive blockIdx round-robin (block
 // b on XCD b % 8); give each XCD a contiguous run of tiles (any grid size: XCD x
-// holds ceil((nblk - x) / 8) blocks).  Default order: (pixel tile, channel tile)
-// pairs, channel tile fastest, so blocks reading the same input pixels share an
-// L2.  DLS_CONV_XCD_COMAJOR=1 (probe knob): channel tile slowest, so an XCD's
-// blocks share its channel tiles' weights instead.
-#ifndef DLS_CONV_XCD_COMAJOR
-#define DLS_CONV_XCD_COMAJOR 0
-#endif
+// holds ceil((nblk - x) / 8) blocks), (pixel tile, channel tile) pairs with the
+// channel tile fastest, so blocks reading the same input pixels share an L2.
+// (Channel tile slowest instead, so an XCD's blocks share weights: null,
+// profiles/r06_conv_ab.txt.)
 __device__ __forceinline__ void tile_of_block(int co_tiles, int &co_t, int &pix_t) {
     const int nblk = gridDim.x, bid = blockIdx.x, x = bid & 7;
     // blocks on XCDs 0..x-1: sum of ceil((nblk - j) / 8)
     const int q = nblk >> 3, rmd = nblk & 7;
     const int t = x * q + (x < rmd ? x : rmd) + (bid >> 3);
-    if (DLS_CONV_XCD_COMAJOR) {
-        const int pix_tiles = nblk / co_tiles;
-        co_t = t / pix_tiles;
-        pix_t = t - co_t * pix_tiles;
-    } else {
-        co_t = t % co_tiles;
-        pix_t = t / co_tiles;
-    }
+    co_t = t % co_tiles;
+    pix_t = t / co_tiles;
 }
 
 // ---------------------------------------------------------------- generic
@@ -424,22 +425,23 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // r05x2): with one bf16 product per k-step instead of three the layers take
 // 65-85 % of their time — the staging, the fragments' LDS reads and the barriers
 // barely overlap the MFMAs at two waves per SIMD.
-template <int WCO, int WPIX, int NHMAX, bool SKEW = false>
-__global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a) {
+template <int WCO, int WPIX, int NHMAX, bool SKEW = false, int BK = kBK, int NPASS = 1, int OCC = 2>
+__global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_halo(ConvArgs a) {
+    constexpr int RB = 4 * BK + 16;
     constexpr int NT = 64 * WCO * WPIX;
     constexpr int BMC = kWaveTile * WCO;
     constexpr int BNP = kWaveTile * WPIX;
-    constexpr int PPR = kBK / 4, HP = kBK / 8, RPP = NT / PPR;
+    constexpr int PPR = BK / 4, HP = BK / 8, RPP = NT / PPR;
     constexpr int NA = BMC / RPP;
     constexpr int HROWS = RPP * NHMAX;  // halo rows the LDS image holds
-    constexpr int HBYTES = HROWS * kRowB + (SKEW ? (HROWS / 16 + 1) * 16 : 0);
-    constexpr int STAGE = HBYTES + 2 * BMC * kRowB;
-    constexpr int EPI = BNP * (4 * BMC + 16);
+    constexpr int HBYTES = HROWS * RB + (SKEW ? (HROWS / 16 + 1) * 16 : 0);
+    constexpr int STAGE = HBYTES + 2 * BMC * RB;
+    constexpr int EPI = BNP * (4 * BMC / NPASS + 16);
     static_assert(NT % PPR == 0 && BMC % RPP == 0, "staging shape");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *halo = smem;
     uint8_t *abuf = smem + HBYTES;
-    auto hoff = [](int hr) { return hr * kRowB + (SKEW ? (hr >> 4) * 16 : 0); };
+    auto hoff = [](int hr) { return hr * RB + (SKEW ? (hr >> 4) * 16 : 0); };
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
@@ -460,7 +462,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     }
 
     const int part = tid % PPR, row0 = tid / PPR;
-    const int poff = part < HP ? part * 8 : kBK + (part - HP) * 8;
+    const int poff = part < HP ? part * 8 : BK + (part - HP) * 8;
     // input pixel of each halo row this thread stages: -1 zero, -2 past the tile
     int hpix[NHMAX];
 #pragma unroll
@@ -483,7 +485,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 
     u32x4 hreg[NHMAX], areg[NA];
     auto hload = [&](int cc) {
-        const int xo = part < HP ? cc * kBK + part * 8 : a.C + cc * kBK + (part - HP) * 8;
+        const int xo = part < HP ? cc * BK + part * 8 : a.C + cc * BK + (part - HP) * 8;
 #pragma unroll
         for (int u = 0; u < NHMAX; ++u)
             hreg[u] = hpix[u] >= 0
@@ -497,7 +499,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
                 *reinterpret_cast<u32x4 *>(halo + hoff(row0 + RPP * u) + poff * 2) = hreg[u];
     };
     auto aload = [&](int cc, int tap) {
-        const int kc = tap * a.C + cc * kBK;
+        const int kc = tap * a.C + cc * BK;
         const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
 #pragma unroll
         for (int u = 0; u < NA; ++u) areg[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     auto astore = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < NA; ++u)
-            *reinterpret_cast<u32x4 *>(abuf + (buf * BMC + row0 + RPP * u) * kRowB + poff * 2) = areg[u];
+            *reinterpret_cast<u32x4 *>(abuf + (buf * BMC + row0 + RPP * u) * RB + poff * 2) = areg[u];
     };
 
     // this lane's output pixels (wp*64 + 32 j + r) as halo rows under tap (0, 0)
@@ -522,7 +524,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 
     WaveAcc acc;
     zero_acc(acc);
-    const int nc = a.C / kBK;
+    const int nc = a.C / BK;
     hload(0);
     aload(0, 0);
     hstore();
@@ -530,15 +532,19 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     __syncthreads();
     int step = 0;
     for (int cc = 0; cc < nc; ++cc) {
-        if (cc + 1 < nc) hload(cc + 1);
-#pragma unroll 1
+#pragma unroll
         for (int tap = 0; tap < 9; ++tap, ++step) {
             const bool last = tap == 8;
             const bool nxt = !last || cc + 1 < nc;
             if (nxt) aload(last ? cc + 1 : cc, last ? 0 : tap + 1);
+            // the next chunk's halo loads go out after tap 0's weight loads, so
+            // that tap 0's weight store does not wait for them (vmcnt counts loads
+            // in issue order); the taps unrolled, so the waits are exact counts
+            // (-3 % per forward with the residual prefetch, profiles/r06_conv_ab.txt)
+            if (tap == 0 && cc + 1 < nc) hload(cc + 1);
             const int ky = tap / 3, kx = tap - 3 * ky;
             const int sh = ky * W2 + kx;
-            mfma_chunk(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * kRowB, halo + hoff(hb[0] + sh),
+            mfma_chunk<BK>(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * RB, halo + hoff(hb[0] + sh),
                        halo + hoff(hb[1] + sh), h);
             if (nxt) astore((step + 1) & 1);
             if (last && cc + 1 < nc) {
@@ -548,7 +554,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
             __syncthreads();
         }
     }
-    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
+    epilogue_lds<BMC, BNP, NT, NPASS>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
 // ------------------------------------------------------------------ stem
@@ -764,10 +770,10 @@ int launch_conv(ConvArgs a, hipStream_t st) {
 
 // The halo kernel when the pixel tile can be whole output rows: returns 1 if
 // launched (or the launch failed: rc set), 0 if the shape does not fit it.
-template <int WCO, int WPIX, int NHMAX, bool SKEW>
+template <int WCO, int WPIX, int NHMAX, bool SKEW, int BK = kBK, int NPASS = 1, int OCC = 2>
 int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
-    constexpr int RPP = 64 * WCO * WPIX / (kBK / 4);
+    constexpr int RPP = 64 * WCO * WPIX / (BK / 4);
     const int H = a.H, W = a.W;
     if (W > BNP || BNP % W) return 0;
     const int TR = H < BNP / W ? H : BNP / W;
@@ -787,8 +793,8 @@ int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     if (blocks > INT32_MAX) return 0;
-    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX, SKEW>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
-                       st, a);
+    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX, SKEW, BK, NPASS, OCC>), dim3((unsigned)blocks),
+                       dim3(64 * WCO * WPIX), 0, st, a);
     rc = check_launch("dls_conv_bn_act_split");
     return 1;
 }

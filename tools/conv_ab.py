@@ -50,42 +50,49 @@ def main():
     for key in sel:
         if key == "stem":
             x = torch.randn(B, 3, 32, 32, device=dev, generator=g)
-            _native._lib = libs[0]
-            w = _native.conv_pack_weights_im2col(torch.randn(64, 3, 3, 3, device=dev, generator=g) / 27 ** 0.5)
+            w32 = torch.randn(64, 3, 3, 3, device=dev, generator=g) / 27 ** 0.5
+            ws = []
+            for L in libs:  # each variant packs its own weights (its layout)
+                _native._lib = L
+                ws.append(_native.conv_pack_weights_im2col(w32))
             consts = torch.cat([torch.zeros(64, device=dev), torch.ones(128, device=dev), torch.zeros(64, device=dev)])
             cases.append(("stem (fused im2col) 3-> 64 k3 s1 H32", 1,
-                          lambda x=x, w=w, c=consts: _native.conv_stem_bn_act(x, w, (3, 3), 1, 1, c)))
+                          lambda vi, x=x, ws=ws, c=consts: _native.conv_stem_bn_act(x, ws[vi], (3, 3), 1, 1, c)))
             continue
         cin, cout, k, s, H, res, cnt = RESNET18_CONVS[int(key)]
         pad = k // 2
         ho = (H + 2 * pad - k) // s + 1
+        w32 = torch.randn(cout, cin, k, k, device=dev, generator=g) / (cin * k * k) ** 0.5
+        ws = []
+        for L in libs:
+            _native._lib = L
+            ws.append(_native.conv_pack_weights(w32))
         _native._lib = libs[0]
-        w = _native.conv_pack_weights(torch.randn(cout, cin, k, k, device=dev, generator=g) / (cin * k * k) ** 0.5)
         consts = torch.cat([torch.randn(cout, device=dev, generator=g) * 0.1, torch.ones(cout, device=dev),
                             torch.ones(cout, device=dev), torch.zeros(cout, device=dev)])
         x = _native.conv_pack_input(torch.randn(B, cin, H, H, device=dev, generator=g).relu_())
         r = _native.conv_pack_input(torch.randn(B, cout, ho, ho, device=dev, generator=g)) if res else None
         cases.append((f"{cin:3d}->{cout:3d} k{k} s{s} H{H:2d} res={int(res)} x{cnt}", cnt,
-                      lambda x=x, w=w, c=consts, r=r, k=k, s=s, pad=pad:
-                      _native.conv_bn_act(x, w, (k, k), s, pad, c, r, True)))
+                      lambda vi, x=x, ws=ws, c=consts, r=r, k=k, s=s, pad=pad:
+                      _native.conv_bn_act(x, ws[vi], (k, k), s, pad, c, r, True)))
     tot = [0.0] * len(libs)
     print(f"batch {B}, {a.rounds} rounds x {a.launches} launches, variants {a.variants}", flush=True)
     for name, cnt, fn in cases:
         outs = []
-        for L in libs:
+        for vi, L in enumerate(libs):
             _native._lib = L
-            outs.append(fn())
+            outs.append(fn(vi))
         same = all(torch.equal(o, outs[0]) for o in outs[1:])
         del outs
         ts = [[] for _ in libs]
         for _ in range(a.rounds):
             for vi, L in enumerate(libs):
                 _native._lib = L
-                fn()
+                fn(vi)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.launches):
-                    fn()
+                    fn(vi)
                 e1.record()
                 torch.cuda.synchronize()
                 ts[vi].append(e0.elapsed_time(e1) / a.launches * 1e3 * 1000 / B)
