@@ -54,6 +54,34 @@ __device__ __forceinline__ void pack_tile(f32x4 v, uint64_t *dst_tile, int32_t *
     if (lane < valid_words) dst_tile[lane] = w;  // a tensor's last tile may end early
 }
 
+// The client-side pack (dls_sign_pack_f32) in the wire's own bit order: in step c
+// (0..3) lane l holds parameter 64c + l of the tile (4-byte loads, each
+// wave-instruction 256 contiguous bytes), so the 64-lane ballot of step c IS the
+// tile's word c (bit j = parameter 64c + j) and no bit interleave is needed:
+// 2 compares per 64 parameters and plane, plus the 8 words' store.  (pack_tile's
+// 16-byte loads need a 4-way bit interleave of the ballots in VALU: 31 VALU
+// instructions per 64 parameters, issue-bound at 0.757 of HBM, profiles/r05_pmc_summary.txt.)
+__device__ __forceinline__ void pack_tile_nat(const float (&x)[4], uint64_t *dst_tile, int32_t *nonternary) {
+    const int lane = __lane_id();
+    uint64_t pos[4], neg[4];
+    int nbad = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const bool nan = x[c] != x[c];
+        pos[c] = __ballot(x[c] > 0.f || nan);
+        neg[c] = __ballot(x[c] < 0.f || nan);
+        if (nonternary) nbad += __popcll(__ballot(!(x[c] == 0.f || x[c] == 1.f || x[c] == -1.f || nan)));
+    }
+    if (nonternary && nbad && lane == 0) atomicAdd(nonternary, nbad);
+    // lane 2c + q stores word [pos_c, neg_c][q]
+    const int m = (lane >> 1) & 3;
+    const bool isneg = lane & 1;
+    uint64_t w = isneg ? neg[0] : pos[0];
+#pragma unroll
+    for (int c = 1; c < 4; ++c) w = m == c ? (isneg ? neg[c] : pos[c]) : w;
+    if (lane < 8) dst_tile[lane] = w;
+}
+
 // grid: x = blocks of 4 waves x kPackTPW tiles, y = client.  Each wave issues
 // the loads of its kPackTPW tiles before packing any (memory-level parallelism).
 // (2, 8, 16 tiles per wave: 0.133, 0.125, 0.132 vs 0.122 ms for 16 ResNet-18 clients,
@@ -69,21 +97,21 @@ __global__ __launch_bounds__(kBlock) void k_sign_pack(const float *__restrict__ 
     const int64_t k = blockIdx.y;
     const int lane = __lane_id();
     const float *row = X + k * ldx;
-    f32x4 v[kPackTPW];
+    float v[kPackTPW][4];
 #pragma unroll
     for (int i = 0; i < kPackTPW; ++i) {
-        const int64_t e = (t0 + i) * 256 + 4 * lane;
-        if (e + 4 <= P) {
-            v[i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(row + e));
+        const int64_t e0 = (t0 + i) * 256 + lane;
+        if ((t0 + i + 1) * 256 <= P) {  // wave-uniform: a whole tile
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[i][c] = __builtin_nontemporal_load(row + e0 + 64 * c);
         } else {
-            v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (int c = 0; c < 4; ++c)
-                if (e + c < P) v[i][c] = row[e + c];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[i][c] = e0 + 64 * c < P ? row[e0 + 64 * c] : 0.f;
         }
     }
 #pragma unroll
     for (int i = 0; i < kPackTPW; ++i)
-        if (t0 + i < ntiles) pack_tile(v[i], planes + k * ldp + (t0 + i) * 8, nonternary);
+        if (t0 + i < ntiles) pack_tile_nat(v[i], planes + k * ldp + (t0 + i) * 8, nonternary);
 }
 
 // ---------------------------------------------------------------- vote
