@@ -278,7 +278,8 @@ def bench_sign(args, dev):
     P, K = layout.P, 1000
     W = _native.sign_words(P)
     g = torch.Generator(device=dev).manual_seed(SEED + 3)
-    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    # the server's store layout: rows of W words at a 128-byte pitch
+    planes = torch.randint(-2**62, 2**62, (K, _native.sign_row_pitch(P)), generator=g, device=dev)
     planes[:, 1::2] &= ~planes[:, 0::2]
     sign_out = torch.empty(P, device=dev)
     vote = torch.empty(W, dtype=torch.int64, device=dev)
@@ -358,7 +359,7 @@ def bench_sign_sharded(args, dev, world, rank):
     P, K = layout.P, 1000
     W = _native.sign_words(P)
     g = torch.Generator(device=dev).manual_seed(SEED + 30 + rank)
-    planes = torch.randint(-2**62, 2**62, (K, W), generator=g, device=dev)
+    planes = torch.randint(-2**62, 2**62, (K, _native.sign_row_pitch(P)), generator=g, device=dev)
     planes[:, 1::2] &= ~planes[:, 0::2]
     counts = torch.empty(P, dtype=torch.int32, device=dev)
     sign_out = torch.empty(P, device=dev)

@@ -27,6 +27,13 @@ def sign_words(P):
     return ((P + 255) // 256) * 8
 
 
+def sign_row_pitch(P):
+    """The row pitch (uint64 words) of a store of sign-plane rows: sign_words(P)
+    rounded up to 128 bytes, so that every row starts on a cache line and the
+    vote's 128-byte-aligned wave ranges never share a line (dls_sign_vote)."""
+    return (sign_words(P) + 15) // 16 * 16
+
+
 class QTile(ctypes.Structure):
     """struct dls_qtile (include/dls_hip.h)."""
 

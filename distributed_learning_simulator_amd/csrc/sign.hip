@@ -304,9 +304,18 @@ __global__ __launch_bounds__(64 * kVoteWPBMax) void k_sign_vote(
     // the last 256-parameter tile (vote 0)
     const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (wave >= nwaves) return;  // wave-uniform
-    // nwaves near-equal ranges (sizes differ by at most one group)
-    const int64_t wlo = wave * vote_groups / nwaves;
-    const int64_t whi = (wave + 1) * vote_groups / nwaves;
+    // nwaves near-equal ranges (sizes differ by at most one group; with G > 1, by
+    // up to 8: every range starts on a multiple of 8 groups = 128 bytes, so on rows
+    // whose pitch is a multiple of 128 bytes (_native.sign_row_pitch) no line is
+    // fetched by two waves: HBM reads 1.028 -> 1.016 x the algorithmic bytes even
+    // with the 64-byte pitch, -1.2 % time, profiles/r06_sign_vote_pmc.txt; the host
+    // sizes G for ranges up to 7 groups longer)
+    int64_t wlo = wave * vote_groups / nwaves;
+    int64_t whi = (wave + 1) * vote_groups / nwaves;
+    if (G > 1) {
+        wlo &= ~(int64_t)7;
+        whi = wave + 1 == nwaves ? vote_groups : whi & ~(int64_t)7;
+    }
     const int64_t gend = min(whi, ngroups);
     HSCounter<CB> cpa[G], cna[G];
     uint64_t nana[G];
@@ -527,13 +536,13 @@ int launch_vote(const uint64_t *planes, int64_t ldp, const int32_t *rows, int K,
         if (kVoteWPC > 0) {
             // exactly kVoteWPC waves per CU, near-equal ranges of up to 64 G groups
             int64_t waves = (int64_t)kVoteWPC * device_cus();
-            int64_t r = (vote_groups + waves - 1) / waves;
+            int64_t r = (vote_groups + waves - 1) / waves + 7;  // + the range alignment
             if (r > 64 * kVoteG) {
                 // models past 64 kVoteG groups per wave (P > ~16.7M on 256 CUs, e.g.
                 // VGG-16): a multiple of kVoteWPC waves per CU, so that every wave
                 // keeps the wide layout (G = kVoteG at most) instead of G = 1
                 waves *= (r + 64 * kVoteG - 1) / (64 * kVoteG);
-                r = (vote_groups + waves - 1) / waves;
+                r = (vote_groups + waves - 1) / waves + 7;
             }
             if (r > 64) {
                 nwaves = waves;

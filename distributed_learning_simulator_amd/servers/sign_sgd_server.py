@@ -42,7 +42,7 @@ class SignSGDServer(Server):
         _native.require_gpu()
         self.sign_gradients: list = []
         self._layout = None
-        self._planes = None  # int64 [K, W] (uint64 words)
+        self._planes = None  # int64 [K, sign_row_pitch(P)] (uint64 words)
         self._X = None  # fp32 staging row for list inputs
         self._bad = None
 
@@ -50,9 +50,9 @@ class SignSGDServer(Server):
         if self._layout is None:
             self._layout = ParameterLayout((str(i), s) for i, s in enumerate(shapes))
             P = self._layout.P
-            W = _native.sign_words(P)
-            self._planes = torch.zeros((self.worker_number, W), dtype=torch.int64,
-                                       device=self.device)
+            # rows of sign_words(P) words at a 128-byte pitch (sign_row_pitch)
+            self._planes = torch.zeros((self.worker_number, _native.sign_row_pitch(P)),
+                                       dtype=torch.int64, device=self.device)
             self._X = torch.zeros((1, P), dtype=torch.float32, device=self.device)
             self._bad = torch.zeros(1, dtype=torch.int32, device=self.device)
         elif [tuple(s) for s in shapes] != self._layout.shapes:
@@ -61,7 +61,8 @@ class SignSGDServer(Server):
     def _store_client(self, slot, sign_gradient):
         if isinstance(sign_gradient, PackedSigns):
             self._ensure(sign_gradient.shapes)
-            self._planes[slot].copy_(sign_gradient.planes, non_blocking=True)
+            self._planes[slot, :sign_gradient.planes.numel()].copy_(sign_gradient.planes,
+                                                                   non_blocking=True)
             return
         shapes = [tuple(t.shape) for t in sign_gradient]
         self._ensure(shapes)

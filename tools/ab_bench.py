@@ -77,14 +77,14 @@ def setup(dev, want=()):
                                                     ptr(out), stream()), 1000 * P * 4 + P * 4)
     if {"vote", "vote_sign", "pack"} & set(want):
         Wd = _native.sign_words(P)
-        planes = torch.randint(-2**62, 2**62, (1000, Wd), generator=g, device=dev)
+        planes = torch.randint(-2**62, 2**62, (1000, _native.sign_row_pitch(P)), generator=g, device=dev)
         planes[:, 1::2] &= ~planes[:, 0::2]
         so = torch.empty(P, device=dev)
         cnt = torch.empty(P, dtype=torch.int32, device=dev)
-        W["vote"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, ptr(cnt), ptr(so),
+        W["vote"] = (lambda L: L.dls_sign_vote(ptr(planes), planes.stride(0), None, 1000, P, ptr(cnt), ptr(so),
                                                None, stream()), 1000 * Wd * 8 + 2 * P * 4)
         vp = torch.empty(Wd, dtype=torch.int64, device=dev)
-        W["vote_sign"] = (lambda L: L.dls_sign_vote(ptr(planes), Wd, None, 1000, P, None, ptr(so),
+        W["vote_sign"] = (lambda L: L.dls_sign_vote(ptr(planes), planes.stride(0), None, 1000, P, None, ptr(so),
                                                     ptr(vp), stream()), 1000 * Wd * 8 + P * 4 + Wd * 8,
                           so)
         X = torch.sign(torch.randn((16, P), generator=g, device=dev))
