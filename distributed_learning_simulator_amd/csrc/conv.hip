@@ -111,11 +111,9 @@ typedef f32x16 WaveAcc[2][2];
 // (this lane's row r of the wave's first 32-channel tile; the second at +32
 // rows), B rows of the two 32-pixel tiles at b0 / b1 (this lane's pixel).
 // Products in the fixed order lo*hi, hi*lo, hi*hi per k-step.
-// BK: channels per chunk (an LDS row holds BK hi, BK lo and a 16-B pad)
-template <int BK = kBK>
 __device__ __forceinline__ void mfma_chunk(WaveAcc &acc, const uint8_t *arow, const uint8_t *b0,
                                            const uint8_t *b1, int h) {
-    constexpr int RB = 4 * BK + 16;
+    constexpr int BK = kBK, RB = kRowB;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
         const int off = 32 * s + 16 * h;  // bytes: k = 16 s + 8 h .. + 7
@@ -425,9 +423,9 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
 // r05x2): with one bf16 product per k-step instead of three the layers take
 // 65-85 % of their time — the staging, the fragments' LDS reads and the barriers
 // barely overlap the MFMAs at two waves per SIMD.
-template <int WCO, int WPIX, int NHMAX, bool SKEW = false, int BK = kBK, int NPASS = 1, int OCC = 2>
-__global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_halo(ConvArgs a) {
-    constexpr int RB = 4 * BK + 16;
+template <int WCO, int WPIX, int NHMAX, bool SKEW = false>
+__global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a) {
+    constexpr int BK = kBK, RB = kRowB;
     constexpr int NT = 64 * WCO * WPIX;
     constexpr int BMC = kWaveTile * WCO;
     constexpr int BNP = kWaveTile * WPIX;
@@ -436,7 +434,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_halo(ConvArgs 
     constexpr int HROWS = RPP * NHMAX;  // halo rows the LDS image holds
     constexpr int HBYTES = HROWS * RB + (SKEW ? (HROWS / 16 + 1) * 16 : 0);
     constexpr int STAGE = HBYTES + 2 * BMC * RB;
-    constexpr int EPI = BNP * (4 * BMC / NPASS + 16);
+    constexpr int EPI = BNP * (4 * BMC + 16);
     static_assert(NT % PPR == 0 && BMC % RPP == 0, "staging shape");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *halo = smem;
@@ -544,7 +542,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_halo(ConvArgs 
             if (tap == 0 && cc + 1 < nc) hload(cc + 1);
             const int ky = tap / 3, kx = tap - 3 * ky;
             const int sh = ky * W2 + kx;
-            mfma_chunk<BK>(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * RB, halo + hoff(hb[0] + sh),
+            mfma_chunk(acc, abuf + ((step & 1) * BMC + wc * kWaveTile + r) * RB, halo + hoff(hb[0] + sh),
                        halo + hoff(hb[1] + sh), h);
             if (nxt) astore((step + 1) & 1);
             if (last && cc + 1 < nc) {
@@ -554,7 +552,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_halo(ConvArgs 
             __syncthreads();
         }
     }
-    epilogue_lds<BMC, BNP, NT, NPASS>(acc, smem, a, co0, pix0, wc, wp, tid);
+    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
 // ------------------------------------------------------------------ stem
@@ -770,10 +768,10 @@ int launch_conv(ConvArgs a, hipStream_t st) {
 
 // The halo kernel when the pixel tile can be whole output rows: returns 1 if
 // launched (or the launch failed: rc set), 0 if the shape does not fit it.
-template <int WCO, int WPIX, int NHMAX, bool SKEW, int BK = kBK, int NPASS = 1, int OCC = 2>
+template <int WCO, int WPIX, int NHMAX, bool SKEW>
 int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
-    constexpr int RPP = 64 * WCO * WPIX / (BK / 4);
+    constexpr int RPP = 64 * WCO * WPIX / (kBK / 4);
     const int H = a.H, W = a.W;
     if (W > BNP || BNP % W) return 0;
     const int TR = H < BNP / W ? H : BNP / W;
@@ -793,8 +791,8 @@ int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     if (blocks > INT32_MAX) return 0;
-    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX, SKEW, BK, NPASS, OCC>), dim3((unsigned)blocks),
-                       dim3(64 * WCO * WPIX), 0, st, a);
+    hipLaunchKernelGGL((k_conv3x3_halo<WCO, WPIX, NHMAX, SKEW>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
+                       st, a);
     rc = check_launch("dls_conv_bn_act_split");
     return 1;
 }
