@@ -555,6 +555,192 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
+// ------------------------------------------- 3x3, stride 1: LDS-DMA pipeline
+// The halo kernel's tiling (whole output rows, one halo tile per 32-channel
+// chunk, the weights of one (chunk, tap) per step) on one 8-wave block per CU,
+// with every operand staged by LDS-DMA (global_load_lds_dwordx4: no staging
+// registers, no ds_write pass) and kept in flight across the barriers:
+//   * weights: a ring of 3 buffers; step t's tile is issued in step t - 2;
+//   * halo: two buffers; chunk c + 1's rows go out during chunk c's taps 0..NHI-1;
+//   * each step waits (counted vmcnt, raw s_barrier) only for what the NEXT step
+//     reads, and each wave reads the next step's first k-step fragments before
+//     the barrier, so the MFMAs resume right after it.
+// LDS rows are 128 B (32 hi + 32 lo bf16) with the 16-B pieces XOR-swizzled by
+// (s >> 1) & 7, s = the row's position in the MFMA lane order (the weight row;
+// for a halo row, the output pixel it is under tap (0, 0) — consecutive along
+// the tile's pixels at every tap): every ds_read_b128 lane group of 16 lanes hits
+// 16 distinct 4-bank groups.  The DMA writes each wave-instruction's 64 pieces
+// lane-linearly, so the swizzle is applied to the lanes' SOURCE addresses.
+// Every output element is reduced in the halo kernel's order (chunks, taps,
+// k-steps, lo*hi, hi*lo, hi*hi): the same bits.
+__device__ __attribute__((aligned(16))) uint32_t kZeroPiece[4];  // source of the halo's padding pieces
+
+__device__ __forceinline__ void glds16(const uint16_t *src, uint8_t *lds_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
+}
+
+constexpr int kWaitLgkm0 = 0xc07f;  // s_waitcnt lgkmcnt(0) (vmcnt, expcnt at their maxima)
+
+template <int NW>
+__device__ __forceinline__ void retire_and_barrier(bool piece_in_flight) {
+    // the step's halo piece (issued after its weights) may stay in flight
+    if (piece_in_flight)
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int WCO, int WPIX, int NHI>
+__global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a) {
+    constexpr int NW = WCO * WPIX, NT = 64 * NW;
+    constexpr int BMC = kWaveTile * WCO, BNP = kWaveTile * WPIX;
+    constexpr int RB = 128;                 // LDS row: 32 hi + 32 lo bf16
+    constexpr int HROWS = 8 * NW * NHI;     // halo rows per buffer (8 rows per wave-instruction)
+    constexpr int HB = HROWS * RB, AB = BMC * RB;
+    constexpr int NAI = BMC / (8 * NW);     // weight DMAs per wave per step
+    constexpr int STAGE = 2 * HB + 3 * AB;
+    constexpr int EPI = BNP * (4 * BMC + 16);
+    static_assert(BMC % (8 * NW) == 0 && NAI >= 1, "weight rows per wave");
+    static_assert(NHI <= 7, "the halo pieces go out in taps 0..6");
+    static_assert(kBK == 32, "128-byte rows");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
+    uint8_t *const hbuf0 = smem;
+    uint8_t *const abuf0 = smem + 2 * HB;
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wc = wv / WPIX, wp = wv % WPIX;
+    int co_t, pt;
+    tile_of_block(a.co_tiles, co_t, pt);
+    const int co0 = co_t * BMC;
+    const int pix0 = pt * BNP;
+    const int W = a.W, H = a.H, W2 = W + 2, TR = a.TR;
+    const int hrows_img = (TR + 2) * W2;
+    int b0, y0;
+    if (TR == H) {
+        b0 = pt * a.TI;
+        y0 = 0;
+    } else {
+        const int tpi = H / TR;
+        b0 = pt / tpi;
+        y0 = (pt - b0 * tpi) * TR;
+    }
+
+    // DMA sources: lane l of a wave-instruction fills slot l & 7 of row l >> 3 of
+    // its 8 rows with the piece (l & 7) ^ swizzle(row)
+    const int sl = lane & 7, lr = lane >> 3;
+    const uint16_t *hsrc[NHI];
+    int hstr[NHI];
+#pragma unroll
+    for (int u = 0; u < NHI; ++u) {
+        const int hr = 8 * (u * NW + wv) + lr;
+        int pix = -1, s = 0;
+        if (hr < a.NH) {
+            const int ti = hr / hrows_img, rem = hr - ti * hrows_img;
+            const int ry = rem / W2, rx = rem - ry * W2;
+            s = ti * TR * W + ry * W + rx;
+            const int b = b0 + ti, iy = y0 - 1 + ry, ix = rx - 1;
+            if (b < a.B && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) pix = (b * H + iy) * W + ix;
+        }
+        const int p = sl ^ ((s >> 1) & 7);
+        hsrc[u] = pix >= 0 ? a.x + (int64_t)pix * (2 * a.C) + ((p & 4) ? a.C : 0) + 8 * (p & 3)
+                           : reinterpret_cast<const uint16_t *>(kZeroPiece);
+        hstr[u] = pix >= 0 ? kBK : 0;
+    }
+    const uint16_t *asrc[NAI];
+#pragma unroll
+    for (int u = 0; u < NAI; ++u) {
+        const int row = 8 * (wv * NAI + u) + lr;
+        const int p = sl ^ ((row >> 1) & 7);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
+    }
+    auto issue_weights = [&](int step, int slot) {  // step's weights into ring slot slot % 3
+        const int cc = step / 9, tap = step - 9 * cc;
+        const int kc = tap * a.C + cc * kBK;
+        uint8_t *dst = abuf0 + (slot % 3) * AB;
+#pragma unroll
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
+    };
+    auto issue_halo = [&](int u, int cc) {
+        glds16(hsrc[u] + cc * hstr[u], hbuf0 + (cc & 1) * HB + (u * NW + wv) * 8 * RB);
+    };
+
+    // fragment addresses: lane (r, h) reads A rows wc*64 + 32 i + r and the halo
+    // rows of pixels wp*64 + 32 j + r
+    const int r = lane & 31, h = lane >> 5;
+    const int fa = (r >> 1) & 7;
+    const int arow = (wc * kWaveTile + r) * RB;
+    int hb[2], pl[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        pl[j] = wp * kWaveTile + 32 * j + r;
+        const int tw = TR * W;
+        const int ti = pl[j] / tw, rem = pl[j] - ti * tw;
+        const int oy = rem / W, ox = rem - oy * W;
+        hb[j] = ti * hrows_img + oy * W2 + ox;
+    }
+    auto frag = [&](Frag &f, int step, int tap, int s) {
+        const uint8_t *ab = abuf0 + (step % 3) * AB + arow;
+        const uint8_t *hbb = hbuf0 + ((step / 9) & 1) * HB;
+        const int qh = 16 * ((2 * s + h) ^ fa), ql = 16 * ((4 + 2 * s + h) ^ fa);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            f.ah[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 32 * RB + qh);
+            f.al[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 32 * RB + ql);
+        }
+        const int ky = tap / 3, kx = tap - 3 * ky;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int hr = hb[j] + ky * W2 + kx;
+            const int fb = ((pl[j] + ky * W + kx) >> 1) & 7;
+            f.bh[j] = *reinterpret_cast<const bf16x8 *>(hbb + hr * RB + 16 * ((2 * s + h) ^ fb));
+            f.bl[j] = *reinterpret_cast<const bf16x8 *>(hbb + hr * RB + 16 * ((4 + 2 * s + h) ^ fb));
+        }
+    };
+
+    WaveAcc acc;
+    zero_acc(acc);
+    const int nc = a.C / kBK, T = 9 * nc;
+#pragma unroll
+    for (int u = 0; u < NHI; ++u) issue_halo(u, 0);
+    issue_weights(0, 0);
+    issue_weights(T > 1 ? 1 : 0, 1);
+    retire_and_barrier<NW>(false);
+    Frag f0, f1;
+    frag(f0, 0, 0, 0);
+    for (int cc = 0; cc < nc; ++cc) {
+        const bool more = cc + 1 < nc;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            // unconditional in every step (the last steps re-load the last
+            // weights into a buffer no later step reads; the fragments past the
+            // last step read stale LDS), so that the compiler's lgkmcnt / vmcnt
+            // counts stay exact
+            const int t = 9 * cc + tap;
+            issue_weights(t + 2 < T ? t + 2 : T - 1, t + 2);
+            const bool piece = more && tap < NHI;
+            if (piece) issue_halo(tap, cc + 1);
+            // the order is pinned: each k-step's reads go out a whole k-step of
+            // MFMAs ahead of their use (left alone, the compiler sinks them next
+            // to their MFMAs to save registers)
+            __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+            frag(f1, t, tap, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_frag(acc, f0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+            frag(f0, t + 1, tap == 8 ? 0 : tap + 1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_frag(acc, f1);
+            retire_and_barrier<NW>(piece);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last fragment read
+    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
+}
+
 // ------------------------------------------------------------------ stem
 // A first layer whose whole reduction is one chunk (KH * KW * C <= kBK: the
 // 3-channel 3x3 stem of a CIFAR ResNet, 27 terms): the im2col is fused — each
@@ -797,6 +983,34 @@ int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     return 1;
 }
 
+// The LDS-DMA pipeline (k_conv3x3_pipe) when its halo tile fits NHI pieces per wave
+template <int WCO, int WPIX, int NHI>
+int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
+    constexpr int BNP = kWaveTile * WPIX;
+    const int H = a.H, W = a.W;
+    if (W > BNP || BNP % W) return 0;
+    const int TR = H < BNP / W ? H : BNP / W;
+    int TI = 1;
+    if (TR == H) {
+        if (BNP % (H * W)) return 0;
+        TI = BNP / (H * W);
+    } else if (H % TR) {
+        return 0;
+    }
+    const int NH = TI * (TR + 2) * (W + 2);
+    if (NH > 8 * WCO * WPIX * NHI) return 0;
+    a.TI = TI;
+    a.TR = TR;
+    a.NH = NH;
+    a.pix_tiles = (a.M + BNP - 1) / BNP;
+    a.co_tiles = a.Cout / (kWaveTile * WCO);
+    const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
+    if (blocks > INT32_MAX) return 0;
+    hipLaunchKernelGGL((k_conv3x3_pipe<WCO, WPIX, NHI>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0, st, a);
+    rc = check_launch("dls_conv_bn_act_split");
+    return 1;
+}
+
 }  // namespace
 }  // namespace dls
 
@@ -894,6 +1108,7 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     // the generic kernel for every shape.
     if (!DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
+        if (wide && (try_launch_pipe<2, 4, 6>(a, st, rc) || try_launch_pipe<2, 4, 7>(a, st, rc))) return rc;
         const bool skew = W <= 16;
         const int hit = wide ? (skew ? try_launch_halo<2, 2, 9, true>(a, st, rc)
                                      : try_launch_halo<2, 2, 9, false>(a, st, rc))

@@ -7,7 +7,8 @@ shape at one batch, on random operands (cdna_hip_programming.md §5.4 rules 24-2
     python tools/conv_ab.py base prio comajor [--batch 10000] [--rounds 5] [--launches 5]
 
 Prints per shape the median time per 1000 images of each variant, whether every
-variant's output is bit-identical to the first's, and the per-forward total
+variant's output is bit-identical to the first's, whether every variant's
+untimed call of each round reproduced its own first output, and the per-forward total
 (each shape weighted by its count in ResNet-18).
 """
 import argparse
@@ -83,12 +84,12 @@ def main():
             _native._lib = L
             outs.append(fn(vi))
         same = all(torch.equal(o, outs[0]) for o in outs[1:])
-        del outs
         ts = [[] for _ in libs]
+        stable = True  # every variant's every untimed call reproduces its first output (a race screen)
         for _ in range(a.rounds):
             for vi, L in enumerate(libs):
                 _native._lib = L
-                fn(vi)
+                stable &= torch.equal(fn(vi), outs[vi])
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.launches):
@@ -101,7 +102,8 @@ def main():
             tot[vi] += cnt * med[vi]
         cells = "  ".join(f"{v}={m:7.1f}" + (f" ({(m / med[0] - 1) * 100:+5.1f}%)" if vi else "")
                           for vi, (v, m) in enumerate(zip(a.variants, med)))
-        print(f"{name}: {cells}  bits-equal {same}", flush=True)
+        del outs
+        print(f"{name}: {cells}  bits-equal {same}  repeatable {stable}", flush=True)
     cells = "  ".join(f"{v}={t:7.1f}" + (f" ({(t / tot[0] - 1) * 100:+5.1f}%)" if vi else "")
                       for vi, (v, t) in enumerate(zip(a.variants, tot)))
     print(f"TOTAL us per 1000 images (every conv of one forward): {cells}", flush=True)
