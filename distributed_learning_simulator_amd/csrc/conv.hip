@@ -49,6 +49,12 @@
 #ifndef DLS_CONV_GENERIC_ONLY
 #define DLS_CONV_GENERIC_ONLY 0
 #endif
+#ifndef DLS_CONV_PIPE_MODE  // probe knob: 0 = no LDS-DMA pipeline
+#define DLS_CONV_PIPE_MODE 1
+#endif
+#ifndef DLS_CONV_PIPE_NARROW  // probe knob: the one-halo-buffer pipeline for 64-channel layers
+#define DLS_CONV_PIPE_NARROW 1
+#endif
 
 namespace dls {
 namespace {
@@ -592,22 +598,26 @@ __device__ __forceinline__ void retire_and_barrier(bool piece_in_flight) {
     asm volatile("" ::: "memory");
 }
 
-template <int WCO, int WPIX, int NHI>
-__global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a) {
+// NHB = 1 (one halo buffer, blocks of <= 80 KB that fit two to a CU): the next
+// chunk's halo is loaded after the chunk's last tap, its latency exposed in this
+// block and covered by the other block on the CU.
+template <int WCO, int WPIX, int NHI, int NHB = 2, int OCC = 1>
+__global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs a) {
     constexpr int NW = WCO * WPIX, NT = 64 * NW;
     constexpr int BMC = kWaveTile * WCO, BNP = kWaveTile * WPIX;
     constexpr int RB = 128;                 // LDS row: 32 hi + 32 lo bf16
     constexpr int HROWS = 8 * NW * NHI;     // halo rows per buffer (8 rows per wave-instruction)
     constexpr int HB = HROWS * RB, AB = BMC * RB;
     constexpr int NAI = BMC / (8 * NW);     // weight DMAs per wave per step
-    constexpr int STAGE = 2 * HB + 3 * AB;
+    constexpr int STAGE = NHB * HB + 3 * AB;
     constexpr int EPI = BNP * (4 * BMC + 16);
     static_assert(BMC % (8 * NW) == 0 && NAI >= 1, "weight rows per wave");
-    static_assert(NHI <= 7, "the halo pieces go out in taps 0..6");
+    static_assert(NHB == 1 || NHI <= 7, "the halo pieces go out in taps 0..6");
+    static_assert(NHB == 1 || NHB == 2, "halo buffers");
     static_assert(kBK == 32, "128-byte rows");
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *const hbuf0 = smem;
-    uint8_t *const abuf0 = smem + 2 * HB;
+    uint8_t *const abuf0 = smem + NHB * HB;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wc = wv / WPIX, wp = wv % WPIX;
@@ -629,9 +639,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a)
 
     // DMA sources: lane l of a wave-instruction fills slot l & 7 of row l >> 3 of
     // its 8 rows with the piece (l & 7) ^ swizzle(row)
+    // a halo DMA lane's source, one register per DMA: input pixel * 8 + piece, or
+    // -1 for the zero piece
     const int sl = lane & 7, lr = lane >> 3;
-    const uint16_t *hsrc[NHI];
-    int hstr[NHI];
+    int hsrc[NHI];
 #pragma unroll
     for (int u = 0; u < NHI; ++u) {
         const int hr = 8 * (u * NW + wv) + lr;
@@ -643,11 +654,13 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a)
             const int b = b0 + ti, iy = y0 - 1 + ry, ix = rx - 1;
             if (b < a.B && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) pix = (b * H + iy) * W + ix;
         }
-        const int p = sl ^ ((s >> 1) & 7);
-        hsrc[u] = pix >= 0 ? a.x + (int64_t)pix * (2 * a.C) + ((p & 4) ? a.C : 0) + 8 * (p & 3)
-                           : reinterpret_cast<const uint16_t *>(kZeroPiece);
-        hstr[u] = pix >= 0 ? kBK : 0;
+        hsrc[u] = pix >= 0 ? pix * 8 + (sl ^ ((s >> 1) & 7)) : -1;
     }
+    // the zero piece's address, opaque to the compiler: computed once, not
+    // re-loaded from the GOT in the loop (a scalar load there would make every
+    // lgkmcnt wait a full drain)
+    const uint16_t *zero = reinterpret_cast<const uint16_t *>(kZeroPiece);
+    asm volatile("" : "+s"(zero));
     const uint16_t *asrc[NAI];
 #pragma unroll
     for (int u = 0; u < NAI; ++u) {
@@ -663,7 +676,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a)
         for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
     };
     auto issue_halo = [&](int u, int cc) {
-        glds16(hsrc[u] + cc * hstr[u], hbuf0 + (cc & 1) * HB + (u * NW + wv) * 8 * RB);
+        const int v = hsrc[u], p = v & 7;
+        const uint16_t *src =
+            v >= 0 ? a.x + (int64_t)(v >> 3) * (2 * a.C) + ((p & 4) ? a.C : 0) + 8 * (p & 3) + cc * kBK : zero;
+        glds16(src, hbuf0 + (NHB == 2 ? (cc & 1) * HB : 0) + (u * NW + wv) * 8 * RB);
     };
 
     // fragment addresses: lane (r, h) reads A rows wc*64 + 32 i + r and the halo
@@ -682,7 +698,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a)
     }
     auto frag = [&](Frag &f, int step, int tap, int s) {
         const uint8_t *ab = abuf0 + (step % 3) * AB + arow;
-        const uint8_t *hbb = hbuf0 + ((step / 9) & 1) * HB;
+        const uint8_t *hbb = hbuf0 + (NHB == 2 ? ((step / 9) & 1) * HB : 0);
         const int qh = 16 * ((2 * s + h) ^ fa), ql = 16 * ((4 + 2 * s + h) ^ fa);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -718,8 +734,8 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a)
             // last step read stale LDS), so that the compiler's lgkmcnt / vmcnt
             // counts stay exact
             const int t = 9 * cc + tap;
+            const bool piece = NHB == 2 && more && tap < NHI;
             issue_weights(t + 2 < T ? t + 2 : T - 1, t + 2);
-            const bool piece = more && tap < NHI;
             if (piece) issue_halo(tap, cc + 1);
             // the order is pinned: each k-step's reads go out a whole k-step of
             // MFMAs ahead of their use (left alone, the compiler sinks them next
@@ -729,11 +745,20 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3_pipe(ConvArgs a)
             __builtin_amdgcn_sched_barrier(0);
             mfma_frag(acc, f0);
             __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-            frag(f0, t + 1, tap == 8 ? 0 : tap + 1, 0);
+            const bool reload = NHB == 1 && tap == 8 && more;  // the next chunk's halo is not in yet
+            if (!reload) {
+                __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+                frag(f0, t + 1, tap == 8 ? 0 : tap + 1, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
             mfma_frag(acc, f1);
             retire_and_barrier<NW>(piece);
+            if (reload) {  // every wave is past its reads of this chunk's halo
+#pragma unroll
+                for (int u = 0; u < NHI; ++u) issue_halo(u, cc + 1);
+                retire_and_barrier<NW>(false);
+                frag(f0, t + 1, 0, 0);
+            }
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -983,8 +1008,8 @@ int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     return 1;
 }
 
-// The LDS-DMA pipeline (k_conv3x3_pipe) when its halo tile fits NHI pieces per wave
-template <int WCO, int WPIX, int NHI>
+// The LDS-DMA pipeline (k_conv3x3_pipe) when the halo tile fits NHI DMAs per wave
+template <int WCO, int WPIX, int NHI, int NHB = 2, int OCC = 1>
 int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
     const int H = a.H, W = a.W;
@@ -998,7 +1023,7 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
         return 0;
     }
     const int NH = TI * (TR + 2) * (W + 2);
-    if (NH > 8 * WCO * WPIX * NHI) return 0;
+    if (NH > 8 * WCO * WPIX * NHI || a.Cout % (kWaveTile * WCO)) return 0;
     a.TI = TI;
     a.TR = TR;
     a.NH = NH;
@@ -1006,7 +1031,8 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     if (blocks > INT32_MAX) return 0;
-    hipLaunchKernelGGL((k_conv3x3_pipe<WCO, WPIX, NHI>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0, st, a);
+    hipLaunchKernelGGL((k_conv3x3_pipe<WCO, WPIX, NHI, NHB, OCC>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
+                       st, a);
     rc = check_launch("dls_conv_bn_act_split");
     return 1;
 }
@@ -1108,7 +1134,10 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     // the generic kernel for every shape.
     if (!DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
-        if (wide && (try_launch_pipe<2, 4, 6>(a, st, rc) || try_launch_pipe<2, 4, 7>(a, st, rc))) return rc;
+        if (DLS_CONV_PIPE_MODE >= 1 && wide &&
+            (try_launch_pipe<2, 4, 6>(a, st, rc) || try_launch_pipe<2, 4, 7>(a, st, rc)))
+            return rc;
+        if (DLS_CONV_PIPE_NARROW && !wide && try_launch_pipe<1, 4, 11, 1, 2>(a, st, rc)) return rc;
         const bool skew = W <= 16;
         const int hit = wide ? (skew ? try_launch_halo<2, 2, 9, true>(a, st, rc)
                                      : try_launch_halo<2, 2, 9, false>(a, st, rc))
