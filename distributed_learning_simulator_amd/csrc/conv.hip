@@ -31,10 +31,15 @@
 // pixel's hi (or lo) channel run.  Each wave owns a 64 x 64 (channel x pixel)
 // output tile = 2 x 2 MFMA tiles; operands are staged in chunks of 32 channels
 // through LDS (register staging, rows padded by 16 B: conflict-free
-// ds_read_b128 fragments).  Two kernels:
-//   k_conv3x3_halo  3x3 stride-1 convolutions: the block's pixels are whole
+// ds_read_b128 fragments).  Kernels:
+//   k_conv3x3_pipe  3x3 stride-1 convolutions: the block's pixels are whole
 //                   output rows, so its input is ONE halo tile staged once per
-//                   channel chunk and read by all 9 taps at shifted rows;
+//                   channel chunk and read by all 9 taps at shifted rows; every
+//                   operand staged by LDS-DMA into XOR-swizzled rows and kept in
+//                   flight across the barriers (a 3-slot weight ring, 1 or 2
+//                   halo buffers);
+//   k_conv3x3_halo  the same tiling register-staged (shapes whose halo tile the
+//                   pipeline's LDS budget does not fit: 4x4 images);
 //   k_conv_bf16x3   anything else (stride 2, 1x1, sizes the halo tiling does
 //                   not fit): every (tap, chunk) gathers its B tile.
 // The epilogue goes through LDS: the raw tile is transposed to [pixel][channel]
@@ -49,11 +54,8 @@
 #ifndef DLS_CONV_GENERIC_ONLY
 #define DLS_CONV_GENERIC_ONLY 0
 #endif
-#ifndef DLS_CONV_PIPE_MODE  // probe knob: 0 = no LDS-DMA pipeline
-#define DLS_CONV_PIPE_MODE 1
-#endif
-#ifndef DLS_CONV_PIPE_NARROW  // probe knob: the one-halo-buffer pipeline for 64-channel layers
-#define DLS_CONV_PIPE_NARROW 1
+#ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
+#define DLS_CONV_PIPE 1
 #endif
 
 namespace dls {
@@ -563,14 +565,18 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 
 // ------------------------------------------- 3x3, stride 1: LDS-DMA pipeline
 // The halo kernel's tiling (whole output rows, one halo tile per 32-channel
-// chunk, the weights of one (chunk, tap) per step) on one 8-wave block per CU,
-// with every operand staged by LDS-DMA (global_load_lds_dwordx4: no staging
-// registers, no ds_write pass) and kept in flight across the barriers:
+// chunk, the weights of one (chunk, tap) per step) with every operand staged by
+// LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass) and
+// kept in flight across the barriers:
 //   * weights: a ring of 3 buffers; step t's tile is issued in step t - 2;
-//   * halo: two buffers; chunk c + 1's rows go out during chunk c's taps 0..NHI-1;
+//   * halo (NHB = 2, an 8-wave block per CU): two buffers; chunk c + 1's rows go
+//     out during chunk c's taps 0..NHI-1;
 //   * each step waits (counted vmcnt, raw s_barrier) only for what the NEXT step
 //     reads, and each wave reads the next step's first k-step fragments before
 //     the barrier, so the MFMAs resume right after it.
+// Per layer against k_conv3x3_halo (profiles/r06_conv_pipe_ab.txt): -7 % on
+// 16x16 (4-wave, NHB = 1), -12 % on 8x8 (8-wave, NHB = 2), -1.5 % on 32x32
+// (64 channels, 4-wave, NHB = 1); the 4x4 layers' halo tiles do not fit.
 // LDS rows are 128 B (32 hi + 32 lo bf16) with the 16-B pieces XOR-swizzled by
 // (s >> 1) & 7, s = the row's position in the MFMA lane order (the weight row;
 // for a halo row, the output pixel it is under tap (0, 0) — consecutive along
@@ -1134,10 +1140,15 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     // the generic kernel for every shape.
     if (!DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
-        if (DLS_CONV_PIPE_MODE >= 1 && wide &&
-            (try_launch_pipe<2, 4, 6>(a, st, rc) || try_launch_pipe<2, 4, 7>(a, st, rc)))
+        // the LDS-DMA pipelines (profiles/r06_conv_pipe_ab.txt): 128-channel
+        // multiples in 4-wave one-halo-buffer blocks two per CU where the halo
+        // tile fits (16x16 images), else in 8-wave double-buffered ones (8x8);
+        // 64 channels in 4-wave one-halo-buffer blocks (32x32)
+        if (DLS_CONV_PIPE && wide &&
+            (try_launch_pipe<2, 2, 6, 1, 2>(a, st, rc) || try_launch_pipe<2, 4, 6>(a, st, rc) ||
+             try_launch_pipe<2, 4, 7>(a, st, rc)))
             return rc;
-        if (DLS_CONV_PIPE_NARROW && !wide && try_launch_pipe<1, 4, 11, 1, 2>(a, st, rc)) return rc;
+        if (DLS_CONV_PIPE && !wide && try_launch_pipe<1, 4, 11, 1, 2>(a, st, rc)) return rc;
         const bool skew = W <= 16;
         const int hit = wide ? (skew ? try_launch_halo<2, 2, 9, true>(a, st, rc)
                                      : try_launch_halo<2, 2, 9, false>(a, st, rc))
