@@ -39,7 +39,7 @@
 //                   flight across the barriers (a 3-slot weight ring, 1 or 2
 //                   halo buffers);
 //   k_conv3x3_halo  the same tiling register-staged (shapes whose halo tile the
-//                   pipeline's LDS budget does not fit: 4x4 images);
+//                   pipeline's LDS budget does not fit; none of ResNet-18's);
 //   k_conv_bf16x3   anything else (stride 2, 1x1, sizes the halo tiling does
 //                   not fit): every (tap, chunk) gathers its B tile.
 // The epilogue goes through LDS: the raw tile is transposed to [pixel][channel]
@@ -574,9 +574,12 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 //   * each step waits (counted vmcnt, raw s_barrier) only for what the NEXT step
 //     reads, and each wave reads the next step's first k-step fragments before
 //     the barrier, so the MFMAs resume right after it.
-// Per layer against k_conv3x3_halo (profiles/r06_conv_pipe_ab.txt): -7 % on
-// 16x16 (4-wave, NHB = 1), -12 % on 8x8 (8-wave, NHB = 2), -1.5 % on 32x32
-// (64 channels, 4-wave, NHB = 1); the 4x4 layers' halo tiles do not fit.
+// The halo tile holds TR + 2 image rows of each of its TI images and no padding
+// columns: a lane whose tap falls left or right of the image reads a zero row
+// kept beside the buffers.  Per layer against k_conv3x3_halo
+// (profiles/r06_conv_pipe_ab.txt): -9 % on 16x16 (4-wave, NHB = 1), -12 % on
+// 8x8 and -14 % on 4x4 (8-wave, NHB = 2), -1 to -2 % on 32x32 (64 channels,
+// 4-wave, NHB = 1).
 // LDS rows are 128 B (32 hi + 32 lo bf16) with the 16-B pieces XOR-swizzled by
 // (s >> 1) & 7, s = the row's position in the MFMA lane order (the weight row;
 // for a halo row, the output pixel it is under tap (0, 0) — consecutive along
@@ -615,7 +618,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     constexpr int HROWS = 8 * NW * NHI;     // halo rows per buffer (8 rows per wave-instruction)
     constexpr int HB = HROWS * RB, AB = BMC * RB;
     constexpr int NAI = BMC / (8 * NW);     // weight DMAs per wave per step
-    constexpr int STAGE = NHB * HB + 3 * AB;
+    constexpr int STAGE = NHB * HB + 3 * AB + RB;  // + the zero row
     constexpr int EPI = BNP * (4 * BMC + 16);
     static_assert(BMC % (8 * NW) == 0 && NAI >= 1, "weight rows per wave");
     static_assert(NHB == 1 || NHI <= 7, "the halo pieces go out in taps 0..6");
@@ -624,6 +627,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *const hbuf0 = smem;
     uint8_t *const abuf0 = smem + NHB * HB;
+    uint8_t *const zrow = abuf0 + 3 * AB;  // what a tap reads left / right of the image
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wc = wv / WPIX, wp = wv % WPIX;
@@ -631,8 +635,8 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     tile_of_block(a.co_tiles, co_t, pt);
     const int co0 = co_t * BMC;
     const int pix0 = pt * BNP;
-    const int W = a.W, H = a.H, W2 = W + 2, TR = a.TR;
-    const int hrows_img = (TR + 2) * W2;
+    const int W = a.W, H = a.H, TR = a.TR;
+    const int hrows_img = (TR + 2) * W;  // TR + 2 image rows, no padding columns
     int b0, y0;
     if (TR == H) {
         b0 = pt * a.TI;
@@ -655,10 +659,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
         int pix = -1, s = 0;
         if (hr < a.NH) {
             const int ti = hr / hrows_img, rem = hr - ti * hrows_img;
-            const int ry = rem / W2, rx = rem - ry * W2;
-            s = ti * TR * W + ry * W + rx;
-            const int b = b0 + ti, iy = y0 - 1 + ry, ix = rx - 1;
-            if (b < a.B && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) pix = (b * H + iy) * W + ix;
+            const int ry = rem / W, rx = rem - ry * W;
+            s = hr - 2 * W * ti;  // = the row's pixel under tap (1, 1): consecutive along a tile
+            const int b = b0 + ti, iy = y0 - 1 + ry;
+            if (b < a.B && (unsigned)iy < (unsigned)H) pix = (b * H + iy) * W + rx;
         }
         hsrc[u] = pix >= 0 ? pix * 8 + (sl ^ ((s >> 1) & 7)) : -1;
     }
@@ -693,14 +697,15 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     const int r = lane & 31, h = lane >> 5;
     const int fa = (r >> 1) & 7;
     const int arow = (wc * kWaveTile + r) * RB;
-    int hb[2], pl[2];
+    int hb[2], pl[2], oxj[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         pl[j] = wp * kWaveTile + 32 * j + r;
         const int tw = TR * W;
         const int ti = pl[j] / tw, rem = pl[j] - ti * tw;
         const int oy = rem / W, ox = rem - oy * W;
-        hb[j] = ti * hrows_img + oy * W2 + ox;
+        hb[j] = ti * hrows_img + oy * W + ox;  // its halo row under tap (0, 1)
+        oxj[j] = ox;
     }
     auto frag = [&](Frag &f, int step, int tap, int s) {
         const uint8_t *ab = abuf0 + (step % 3) * AB + arow;
@@ -714,16 +719,19 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
         const int ky = tap / 3, kx = tap - 3 * ky;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int hr = hb[j] + ky * W2 + kx;
-            const int fb = ((pl[j] + ky * W + kx) >> 1) & 7;
-            f.bh[j] = *reinterpret_cast<const bf16x8 *>(hbb + hr * RB + 16 * ((2 * s + h) ^ fb));
-            f.bl[j] = *reinterpret_cast<const bf16x8 *>(hbb + hr * RB + 16 * ((4 + 2 * s + h) ^ fb));
+            const int sh = ky * W + kx - 1;
+            const bool in = (unsigned)(oxj[j] + kx - 1) < (unsigned)W;
+            const int fb = ((pl[j] + sh) >> 1) & 7;
+            const uint8_t *row = in ? hbb + (hb[j] + sh) * RB : zrow;
+            f.bh[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((2 * s + h) ^ fb));
+            f.bl[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((4 + 2 * s + h) ^ fb));
         }
     };
 
     WaveAcc acc;
     zero_acc(acc);
     const int nc = a.C / kBK, T = 9 * nc;
+    if (tid < RB / 16) *reinterpret_cast<u32x4 *>(zrow + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int u = 0; u < NHI; ++u) issue_halo(u, 0);
     issue_weights(0, 0);
@@ -1028,7 +1036,7 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     } else if (H % TR) {
         return 0;
     }
-    const int NH = TI * (TR + 2) * (W + 2);
+    const int NH = TI * (TR + 2) * W;  // halo rows without the padding columns
     if (NH > 8 * WCO * WPIX * NHI || a.Cout % (kWaveTile * WCO)) return 0;
     a.TI = TI;
     a.TR = TR;
@@ -1142,13 +1150,13 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
         int rc = DLS_OK;
         // the LDS-DMA pipelines (profiles/r06_conv_pipe_ab.txt): 128-channel
         // multiples in 4-wave one-halo-buffer blocks two per CU where the halo
-        // tile fits (16x16 images), else in 8-wave double-buffered ones (8x8);
-        // 64 channels in 4-wave one-halo-buffer blocks (32x32)
+        // tile fits (16x16 images), else in 8-wave double-buffered ones (8x8,
+        // 4x4); 64 channels in 4-wave one-halo-buffer blocks (32x32)
         if (DLS_CONV_PIPE && wide &&
-            (try_launch_pipe<2, 2, 6, 1, 2>(a, st, rc) || try_launch_pipe<2, 4, 6>(a, st, rc) ||
-             try_launch_pipe<2, 4, 7>(a, st, rc)))
+            (try_launch_pipe<2, 2, 5, 1, 2>(a, st, rc) || try_launch_pipe<2, 4, 5>(a, st, rc) ||
+             try_launch_pipe<2, 4, 6>(a, st, rc)))
             return rc;
-        if (DLS_CONV_PIPE && !wide && try_launch_pipe<1, 4, 11, 1, 2>(a, st, rc)) return rc;
+        if (DLS_CONV_PIPE && !wide && try_launch_pipe<1, 4, 10, 1, 2>(a, st, rc)) return rc;
         const bool skew = W <= 16;
         const int hit = wide ? (skew ? try_launch_halo<2, 2, 9, true>(a, st, rc)
                                      : try_launch_halo<2, 2, 9, false>(a, st, rc))
