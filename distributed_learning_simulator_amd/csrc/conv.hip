@@ -1149,11 +1149,12 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     if (!DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
         // the LDS-DMA pipelines (profiles/r06_conv_pipe_ab.txt): 128-channel
-        // multiples in 4-wave one-halo-buffer blocks two per CU where the halo
-        // tile fits (16x16 images), else in 8-wave double-buffered ones (8x8,
-        // 4x4); 64 channels in 4-wave one-halo-buffer blocks (32x32)
+        // multiples in 4-wave one-halo-buffer blocks two per CU on images at
+        // least 16 wide (16x16: -1 to -2 %; 8x8: +0.5 to +1.4 %), else in 8-wave
+        // double-buffered ones (8x8, 4x4); 64 channels in 4-wave one-halo-buffer
+        // blocks (32x32)
         if (DLS_CONV_PIPE && wide &&
-            (try_launch_pipe<2, 2, 5, 1, 2>(a, st, rc) || try_launch_pipe<2, 4, 5>(a, st, rc) ||
+            ((W >= 16 && try_launch_pipe<2, 2, 5, 1, 2>(a, st, rc)) || try_launch_pipe<2, 4, 5>(a, st, rc) ||
              try_launch_pipe<2, 4, 6>(a, st, rc)))
             return rc;
         if (DLS_CONV_PIPE && !wide && try_launch_pipe<1, 4, 10, 1, 2>(a, st, rc)) return rc;
