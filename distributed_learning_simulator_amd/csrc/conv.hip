@@ -618,7 +618,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     constexpr int HROWS = 8 * NW * NHI;     // halo rows per buffer (8 rows per wave-instruction)
     constexpr int HB = HROWS * RB, AB = BMC * RB;
     constexpr int NAI = BMC / (8 * NW);     // weight DMAs per wave per step
-    constexpr int STAGE = NHB * HB + 3 * AB + RB;  // + the zero row
+    constexpr int STAGE = NHB * HB + 3 * AB + 2 * RB;  // + the zero rows
     constexpr int EPI = BNP * (4 * BMC + 16);
     static_assert(BMC % (8 * NW) == 0 && NAI >= 1, "weight rows per wave");
     static_assert(NHB == 1 || NHI <= 7, "the halo pieces go out in taps 0..6");
@@ -627,7 +627,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
     uint8_t *const hbuf0 = smem;
     uint8_t *const abuf0 = smem + NHB * HB;
-    uint8_t *const zrow = abuf0 + 3 * AB;  // what a tap reads left / right of the image
+    // what a tap reads left / right of the image: two zero rows (256-B aligned),
+    // each lane reading the one of its row's parity, so that it hits the banks a
+    // halo row of its position would (no conflicts with the other lanes)
+    uint8_t *const zrow = abuf0 + 3 * AB;
 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wc = wv / WPIX, wp = wv % WPIX;
@@ -697,16 +700,18 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     const int r = lane & 31, h = lane >> 5;
     const int fa = (r >> 1) & 7;
     const int arow = (wc * kWaveTile + r) * RB;
-    int hb[2], pl[2], oxj[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        pl[j] = wp * kWaveTile + 32 * j + r;
+    // pixel tile 1 is tile 0 shifted by 32 pixels: W divides 32 (try_launch_pipe),
+    // so it has tile 0's columns, and its halo rows sit a block-uniform dhb further
+    int hb0, pl0, ox0;
+    {
+        pl0 = wp * kWaveTile + r;
         const int tw = TR * W;
-        const int ti = pl[j] / tw, rem = pl[j] - ti * tw;
-        const int oy = rem / W, ox = rem - oy * W;
-        hb[j] = ti * hrows_img + oy * W + ox;  // its halo row under tap (0, 1)
-        oxj[j] = ox;
+        const int ti = pl0 / tw, rem = pl0 - ti * tw;
+        const int oy = rem / W;
+        ox0 = rem - oy * W;
+        hb0 = ti * hrows_img + oy * W + ox0;  // its halo row under tap (0, 1)
     }
+    const int dhb = TR * W >= 32 ? 32 : (32 / (TR * W)) * hrows_img;
     auto frag = [&](Frag &f, int step, int tap, int s) {
         const uint8_t *ab = abuf0 + (step % 3) * AB + arow;
         const uint8_t *hbb = hbuf0 + (NHB == 2 ? ((step / 9) & 1) * HB : 0);
@@ -717,12 +722,12 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
             f.al[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 32 * RB + ql);
         }
         const int ky = tap / 3, kx = tap - 3 * ky;
+        const int sh = ky * W + kx - 1;
+        const bool in = (unsigned)(ox0 + kx - 1) < (unsigned)W;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int sh = ky * W + kx - 1;
-            const bool in = (unsigned)(oxj[j] + kx - 1) < (unsigned)W;
-            const int fb = ((pl[j] + sh) >> 1) & 7;
-            const uint8_t *row = in ? hbb + (hb[j] + sh) * RB : zrow;
+            const int fb = ((pl0 + 32 * j + sh) >> 1) & 7;
+            const uint8_t *row = in ? hbb + (hb0 + j * dhb + sh) * RB : zrow + ((pl0 + sh) & 1) * RB;
             f.bh[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((2 * s + h) ^ fb));
             f.bl[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((4 + 2 * s + h) ^ fb));
         }
@@ -731,7 +736,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     WaveAcc acc;
     zero_acc(acc);
     const int nc = a.C / kBK, T = 9 * nc;
-    if (tid < RB / 16) *reinterpret_cast<u32x4 *>(zrow + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
+    if (tid < 2 * RB / 16) *reinterpret_cast<u32x4 *>(zrow + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int u = 0; u < NHI; ++u) issue_halo(u, 0);
     issue_weights(0, 0);
@@ -1027,7 +1032,7 @@ template <int WCO, int WPIX, int NHI, int NHB = 2, int OCC = 1>
 int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
     const int H = a.H, W = a.W;
-    if (W > BNP || BNP % W) return 0;
+    if (32 % W) return 0;  // a wave's two 32-pixel tiles share their columns
     const int TR = H < BNP / W ? H : BNP / W;
     int TI = 1;
     if (TR == H) {
@@ -1036,6 +1041,8 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     } else if (H % TR) {
         return 0;
     }
+    // pixel tile 1 = tile 0 + 32 pixels in the same image tile, or whole images on
+    if (TR * W >= 32 ? (TR * W) % 64 : 32 % (TR * W)) return 0;
     const int NH = TI * (TR + 2) * W;  // halo rows without the padding columns
     if (NH > 8 * WCO * WPIX * NHI || a.Cout % (kWaveTile * WCO)) return 0;
     a.TI = TI;
