@@ -22,12 +22,13 @@ pytestmark = pytest.mark.gpu
 dev = torch.device("cuda", 0)
 TOL = 5e-5
 
-# (cin, cout, k, stride, H, W, residual, batch): every ResNet-18 shape (halo kernel
-# for 3x3 stride 1, generic kernel otherwise), ragged last tiles (batch not a
-# multiple of the images per tile), sizes the halo tiling does not fit (28x28,
-# 7x7, 12x12 -> generic), Cout a multiple of 64 but not of 128, a non-square
-# image, and the stem (cin < 32: im2col + the generic kernel, and the fused-im2col
-# stem kernel, which must give the same bits)
+# (cin, cout, k, stride, H, W, residual, batch): every ResNet-18 shape (the LDS-DMA
+# pipeline for 3x3 stride 1, the generic kernel otherwise), ragged last tiles
+# (batch not a multiple of the images per tile), sizes the pipeline does not take
+# (28x28 -> the register-staged halo kernel; 7x7, 12x12 -> generic), Cout a
+# multiple of 64 but not of 128, a non-square image, and the stem (cin < 32:
+# im2col + the generic kernel, and the fused-im2col stem kernel, which must give
+# the same bits)
 SHAPES = [
     (3, 64, 3, 1, 32, 32, False, 4), (64, 64, 3, 1, 32, 32, False, 3), (64, 64, 3, 1, 32, 32, True, 2),
     (64, 128, 3, 2, 32, 32, False, 3), (64, 128, 1, 2, 32, 32, False, 3),
@@ -38,6 +39,13 @@ SHAPES = [
     # stems off the 3x3 / 3-channel fast path: a 5x5 MNIST-like one (runtime
     # index arithmetic) and a strided one over two 64-channel output tiles
     (1, 64, 5, 1, 28, 28, False, 2), (3, 128, 3, 2, 32, 32, False, 2),
+    # the LDS-DMA pipeline's other cases: one channel chunk (32 channels, no
+    # halo reload), 64-channel blocks over 16x16 / 8x8 images (whole images,
+    # partial last tile), 128 channels over 32x32 (4 row tiles per image), a
+    # 24-row image (row tiles at y0 > 0, 4-wave blocks), 4x4 images with two
+    # chunks and a mostly empty tile (48 of 256 pixels)
+    (32, 64, 3, 1, 32, 32, True, 2), (64, 64, 3, 1, 16, 16, False, 3), (64, 64, 3, 1, 8, 8, True, 3),
+    (128, 128, 3, 1, 32, 32, False, 2), (32, 128, 3, 1, 24, 16, True, 2), (64, 256, 3, 1, 4, 4, False, 3),
 ]
 
 
