@@ -54,6 +54,9 @@
 #ifndef DLS_CONV_GENERIC_ONLY
 #define DLS_CONV_GENERIC_ONLY 0
 #endif
+#ifndef DLS_CONV_PHASE  // probe knob: 0 = the generic kernel for 3x3 stride-2 shapes
+#define DLS_CONV_PHASE 1
+#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -785,6 +788,192 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
+// --------------------------------------------- 3x3, stride 2, pad 1: phases
+// A stride-2 3x3 convolution is four stride-1 ones over the input's row / column
+// parity images P_ab(q, r) = x(2q + a, 2r + b), each Ho x Wo: tap (ky, kx) reads
+// P_ab with a = (ky + 1) & 1, b = (kx + 1) & 1 at (oy + dq, ox + dr), dq = -1 for
+// ky = 0 (else 0), dr = -1 for kx = 0.  Phase (1,1) has taps (0,0) (0,2) (2,0)
+// (2,2), (1,0) has (0,1) (2,1), (0,1) has (1,0) (1,2), (0,0) has (1,1).  Each
+// phase's halo is TI x (TR + 1) x Wo rows (output tile + one row above; no
+// padding columns: a tap left of the image reads a zero row), so each input pixel
+// is staged once per channel chunk — the gather kernel stages 2.25 per output
+// pixel per chunk, 9 B tiles.  k_conv3x3_pipe's machinery otherwise: 8-wave
+// blocks, LDS-DMA into swizzled 128-B rows, a 3-slot weight ring two steps ahead,
+// two halo buffers (phase g + 1's rows go out in phase g's first step); the next
+// step's first fragments are read before the barrier within a phase, after it
+// across phases (the next phase's halo lands by the phase's end).  Reduction
+// order: chunks, phases, taps, k-steps — deterministic, not the generic
+// kernel's bits.
+__device__ constexpr int kPhaseTap[9] = {0, 2, 6, 8, 1, 7, 3, 5, 4};  // step -> tap (ky * 3 + kx)
+
+template <int WCO, int WPIX, int NHI>
+__global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs a) {
+    constexpr int NW = WCO * WPIX, NT = 64 * NW;
+    constexpr int BMC = kWaveTile * WCO, BNP = kWaveTile * WPIX;
+    constexpr int RB = 128;
+    constexpr int HROWS = 8 * NW * NHI;
+    constexpr int HB = HROWS * RB, AB = BMC * RB;
+    constexpr int NAI = BMC / (8 * NW);
+    constexpr int STAGE = 2 * HB + 3 * AB + 2 * RB;
+    constexpr int EPI = BNP * (4 * BMC + 16);
+    static_assert(BMC % (8 * NW) == 0 && NAI >= 1, "weight rows per wave");
+    static_assert(kBK == 32, "128-byte rows");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
+    uint8_t *const hbuf0 = smem;
+    uint8_t *const abuf0 = smem + 2 * HB;
+    uint8_t *const zrow = abuf0 + 3 * AB;  // two zero rows, read by parity (k_conv3x3_pipe)
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wc = wv / WPIX, wp = wv % WPIX;
+    int co_t, pt;
+    tile_of_block(a.co_tiles, co_t, pt);
+    const int co0 = co_t * BMC;
+    const int pix0 = pt * BNP;
+    const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, TR = a.TR;
+    const int hrows_img = (TR + 1) * Wo;
+    int b0, y0;
+    if (TR == Ho) {
+        b0 = pt * a.TI;
+        y0 = 0;
+    } else {
+        const int tpi = Ho / TR;
+        b0 = pt / tpi;
+        y0 = (pt - b0 * tpi) * TR;
+    }
+
+    // halo DMA lane sources: the input pixel of phase (1,1) — (2q + 1, 2r + 1) —
+    // or -1, and the piece; phase (a, b) reads (2q + a, 2r + b), 1 - a rows and
+    // 1 - b columns back
+    const int sl = lane & 7, lr = lane >> 3;
+    int hpix[NHI], hpc[NHI];
+#pragma unroll
+    for (int u = 0; u < NHI; ++u) {
+        const int hr = 8 * (u * NW + wv) + lr;
+        int v = -1, s = 0;
+        if (hr < a.NH) {
+            const int ti = hr / hrows_img, rem = hr - ti * hrows_img;
+            const int qq = rem / Wo, r = rem - qq * Wo;
+            const int b = b0 + ti, q = y0 - 1 + qq;
+            s = hr - ti * Wo;  // the row's pixel under dq = -1: consecutive along a tile
+            if (b < a.B && q >= 0) v = (b * H + 2 * q + 1) * W + 2 * r + 1;
+        }
+        hpix[u] = v;
+        hpc[u] = sl ^ ((s >> 1) & 7);
+    }
+    const uint16_t *zero = reinterpret_cast<const uint16_t *>(kZeroPiece);
+    asm volatile("" : "+s"(zero));
+    const uint16_t *asrc[NAI];
+#pragma unroll
+    for (int u = 0; u < NAI; ++u) {
+        const int row = 8 * (wv * NAI + u) + lr;
+        const int p = sl ^ ((row >> 1) & 7);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
+    }
+    auto issue_weights = [&](int step, int slot) {
+        const int cc = step / 9, tap = kPhaseTap[step - 9 * cc];
+        const int kc = tap * a.C + cc * kBK;
+        uint8_t *dst = abuf0 + (slot % 3) * AB;
+#pragma unroll
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
+    };
+    // phase g = 4 cc + p (p: 0 = (1,1), 1 = (1,0), 2 = (0,1), 3 = (0,0)) into buffer g & 1
+    auto issue_halo = [&](int g) {
+        const int cc = g >> 2, p = g & 3;
+        const int back = (p < 2 ? 0 : W) + ((p & 1) ? 1 : 0);  // (1 - a) rows + (1 - b) columns
+#pragma unroll
+        for (int u = 0; u < NHI; ++u) {
+            const int v = hpix[u], pc = hpc[u];
+            const uint16_t *src =
+                v >= 0 ? a.x + (int64_t)(v - back) * (2 * a.C) + ((pc & 4) ? a.C : 0) + 8 * (pc & 3) + cc * kBK
+                       : zero;
+            glds16(src, hbuf0 + (g & 1) * HB + (u * NW + wv) * 8 * RB);
+        }
+    };
+
+    const int r = lane & 31, h = lane >> 5;
+    const int fa = (r >> 1) & 7;
+    const int arow = (wc * kWaveTile + r) * RB;
+    int hb0, pl0, ox0;
+    {
+        pl0 = wp * kWaveTile + r;
+        const int tw = TR * Wo;
+        const int ti = pl0 / tw, rem = pl0 - ti * tw;
+        const int oy = rem / Wo;
+        ox0 = rem - oy * Wo;
+        hb0 = ti * hrows_img + oy * Wo + ox0;  // its halo row under dq = -1, dr = 0
+    }
+    const int dhb = TR * Wo >= 32 ? 32 : (32 / (TR * Wo)) * hrows_img;
+    auto frag = [&](Frag &f, int step, int s) {
+        const int cc = step / 9, k = step - 9 * cc;
+        const int tap = kPhaseTap[k], g = 4 * cc + (k < 4 ? 0 : k < 6 ? 1 : k < 8 ? 2 : 3);
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const uint8_t *ab = abuf0 + (step % 3) * AB + arow;
+        const uint8_t *hbb = hbuf0 + (g & 1) * HB;
+        const int qh = 16 * ((2 * s + h) ^ fa), ql = 16 * ((4 + 2 * s + h) ^ fa);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            f.ah[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 32 * RB + qh);
+            f.al[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 32 * RB + ql);
+        }
+        const int sh = (ky == 0 ? 0 : Wo) + (kx == 0 ? -1 : 0);  // (1 + dq) * Wo + dr
+        const bool in = kx != 0 || ox0 > 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int fb = ((pl0 + 32 * j + sh) >> 1) & 7;
+            const uint8_t *row = in ? hbb + (hb0 + j * dhb + sh) * RB : zrow + ((pl0 + sh) & 1) * RB;
+            f.bh[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((2 * s + h) ^ fb));
+            f.bl[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((4 + 2 * s + h) ^ fb));
+        }
+    };
+
+    WaveAcc acc;
+    zero_acc(acc);
+    const int nc = a.C / kBK, T = 9 * nc;
+    if (tid < 2 * RB / 16) *reinterpret_cast<u32x4 *>(zrow + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
+    issue_halo(0);
+    issue_weights(0, 0);
+    issue_weights(T > 1 ? 1 : 0, 1);
+    retire_and_barrier<NW>(false);
+    Frag f0, f1;
+    frag(f0, 0, 0);
+    for (int cc = 0; cc < nc; ++cc) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int t = 9 * cc + k;
+            const bool first = k == 0 || k == 4 || k == 6 || k == 8;  // a phase's first step
+            const bool last = k == 3 || k == 5 || k == 7 || k == 8;   // a phase's last step
+            const int g = 4 * cc + (k < 4 ? 0 : k < 6 ? 1 : k < 8 ? 2 : 3);
+            issue_weights(t + 2 < T ? t + 2 : T - 1, t + 2);
+            // the next phase's halo into the buffer the previous phase read (every
+            // wave is past its last read of it: the barrier before this phase)
+            if (first && g + 1 < 4 * nc) issue_halo(g + 1);
+            __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+            frag(f1, t, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_frag(acc, f0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!last) {
+                __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+                frag(f0, t + 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_frag(acc, f1);
+            // this step's weights retired; the next phase's halo (issued after them
+            // in the phase's first step) stays in flight until the phase's last step
+            if (first && !last && g + 1 < 4 * nc)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NHI) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (last) frag(f0, t + 1, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last fragment read
+    epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
+}
+
 // ------------------------------------------------------------------ stem
 // A first layer whose whole reduction is one chunk (KH * KW * C <= kBK: the
 // 3-channel 3x3 stem of a CIFAR ResNet, 27 terms): the im2col is fused — each
@@ -1027,6 +1216,37 @@ int try_launch_halo(ConvArgs a, hipStream_t st, int &rc) {
     return 1;
 }
 
+// The stride-2 phase pipeline (k_conv3x3s2_phase) when its phase halos fit NHI
+// DMAs per wave
+template <int WCO, int WPIX, int NHI>
+int try_launch_phase(ConvArgs a, hipStream_t st, int &rc) {
+    constexpr int BNP = kWaveTile * WPIX;
+    const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo;
+    if ((H | W) & 1 || 2 * Ho != H || 2 * Wo != W || 32 % Wo || a.Cout % (kWaveTile * WCO)) return 0;
+    if ((int64_t)a.B * H * W >= (1ll << 30)) return 0;  // input pixel indices in 32 bits
+    const int TR = Ho < BNP / Wo ? Ho : BNP / Wo;
+    int TI = 1;
+    if (TR == Ho) {
+        if (BNP % (Ho * Wo)) return 0;
+        TI = BNP / (Ho * Wo);
+    } else if (Ho % TR) {
+        return 0;
+    }
+    if (TR * Wo >= 32 ? (TR * Wo) % 64 : 32 % (TR * Wo)) return 0;
+    const int NH = TI * (TR + 1) * Wo;
+    if (NH > 8 * WCO * WPIX * NHI) return 0;
+    a.TI = TI;
+    a.TR = TR;
+    a.NH = NH;
+    a.pix_tiles = (a.M + BNP - 1) / BNP;
+    a.co_tiles = a.Cout / (kWaveTile * WCO);
+    const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
+    if (blocks > INT32_MAX) return 0;
+    hipLaunchKernelGGL((k_conv3x3s2_phase<WCO, WPIX, NHI>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0, st, a);
+    rc = check_launch("dls_conv_bn_act_split");
+    return 1;
+}
+
 // The LDS-DMA pipeline (k_conv3x3_pipe) when the halo tile fits NHI DMAs per wave
 template <int WCO, int WPIX, int NHI, int NHB = 2, int OCC = 1>
 int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
@@ -1171,6 +1391,10 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
                              : (skew ? try_launch_halo<1, 4, 11, true>(a, st, rc)
                                      : try_launch_halo<1, 4, 11, false>(a, st, rc));
         if (hit) return rc;
+    }
+    if (DLS_CONV_PHASE && !DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 2 && pad == 1 && wide) {
+        int rc = DLS_OK;
+        if (try_launch_phase<2, 4, 5>(a, st, rc)) return rc;
     }
     return wide ? launch_conv<2, 2>(a, st) : launch_conv<1, 4>(a, st);
 }

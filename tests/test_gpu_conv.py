@@ -46,6 +46,9 @@ SHAPES = [
     # chunks and a mostly empty tile (48 of 256 pixels)
     (32, 64, 3, 1, 32, 32, True, 2), (64, 64, 3, 1, 16, 16, False, 3), (64, 64, 3, 1, 8, 8, True, 3),
     (128, 128, 3, 1, 32, 32, False, 2), (32, 128, 3, 1, 24, 16, True, 2), (64, 256, 3, 1, 4, 4, False, 3),
+    # the stride-2 phase pipeline: a non-square image with a residual (two images
+    # per tile), a partial tile, and a size it does not take (6-wide output)
+    (64, 128, 3, 2, 16, 32, True, 3), (32, 256, 3, 2, 8, 8, False, 5), (128, 128, 3, 2, 12, 12, False, 2),
 ]
 
 
