@@ -57,6 +57,9 @@
 #ifndef DLS_CONV_PHASE  // probe knob: 0 = the generic kernel for 3x3 stride-2 shapes
 #define DLS_CONV_PHASE 1
 #endif
+#ifndef DLS_STEM_WINDOW  // probe knob: 0 = the stem's 27 terms gathered from global memory
+#define DLS_STEM_WINDOW 1
+#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -989,20 +992,46 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs
 // 37 KB per block, 4 blocks per CU (the LDS-staged weights and one 64-channel
 // epilogue pass: 70 KB, 2 blocks).  The same products in the same order and the
 // same epilogue arithmetic: the same bits.
-template <int WPIX, int CIN = 0, int KHW = 0>
+// XT (3 channels, 3x3, stride 1, pad 1, 32-wide images, 8 rows per tile): the
+// block's input window (3 x 10 rows x 34 columns, zero outside the image) is
+// staged in LDS by one 16-B load per thread and the 27 terms gathered from there,
+// instead of 27 scalar loads per thread from global memory; the same values.
+constexpr int kStemWinRow = 40;  // floats per window row: image column ix at ix + 4
+template <int WPIX, int CIN = 0, int KHW = 0, bool XT = false>
 __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float *__restrict__ x) {
     constexpr int NT = 64 * WPIX, BNP = kWaveTile * WPIX;
     constexpr int STAGE = BNP * kRowB;
     constexpr int EPI = BNP * (4 * kWaveTile / 2 + 16);  // two epilogue passes
+    constexpr int WIN = XT ? 3 * 10 * kStemWinRow * 4 : 0;
     static_assert(NT == BNP, "one pixel row per thread");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
+    static_assert(!XT || (CIN == 3 && KHW == 3 && BNP == 256), "the staged window's shape");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[(STAGE > EPI ? STAGE : EPI) + WIN];
     uint8_t *Bs = smem;
+    float *win = reinterpret_cast<float *>(smem + (STAGE > EPI ? STAGE : EPI));
     const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     int co_t, pix_t;
     tile_of_block(a.co_tiles, co_t, pix_t);
     const int co0 = co_t * kWaveTile;
     const int pix0 = pix_t * BNP;
+    if constexpr (XT) {  // rows oy0 - 1 .. oy0 + 8 of the tile's image, 8 columns x 4 per thread
+        const int b = pix0 / (a.H * 32), oy0 = (pix0 - b * a.H * 32) / 32;
+        if (tid < 240) {
+            const int ci = tid / 80, rem = tid - ci * 80, wy = rem / 8, c4 = rem - wy * 8;
+            const int iy = oy0 - 1 + wy;
+            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (b < a.B && (unsigned)iy < (unsigned)a.H)
+                v = *reinterpret_cast<const f32x4 *>(x + (((int64_t)b * 3 + ci) * a.H + iy) * 32 + 4 * c4);
+            *reinterpret_cast<f32x4 *>(win + (ci * 10 + wy) * kStemWinRow + 4 + 4 * c4) = v;
+        } else if (tid < 240 + 15) {  // the padding columns (image columns -1 and 32) of 30 rows
+            const int q = tid - 240;
+            win[(2 * q) * kStemWinRow + 3] = 0.f;
+            win[(2 * q) * kStemWinRow + 36] = 0.f;
+            win[(2 * q + 1) * kStemWinRow + 3] = 0.f;
+            win[(2 * q + 1) * kStemWinRow + 36] = 0.f;
+        }
+        __syncthreads();
+    }
     // A fragments of both k-steps (in flight during the gather): channel tile i,
     // lane row co0 + 32 i + r, k = 16 s + 8 h .. + 7 (hi), + K (lo)
     Frag f[kBK / 16];
@@ -1031,9 +1060,13 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
                 if (k < nk) {
                     const int tap = k / C, ci = k - tap * C;
                     const int ky = tap / KW, kx = tap - ky * KW;
-                    const int iy = oy * a.stride - a.pad + ky, ix = ox * a.stride - a.pad + kx;
-                    if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-                        v = x[(((int64_t)b * C + ci) * a.H + iy) * a.W + ix];
+                    if constexpr (XT) {
+                        v = win[(ci * 10 + (tid >> 5) + ky) * kStemWinRow + ox + kx + 3];
+                    } else {
+                        const int iy = oy * a.stride - a.pad + ky, ix = ox * a.stride - a.pad + kx;
+                        if ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                            v = x[(((int64_t)b * C + ci) * a.H + iy) * a.W + ix];
+                    }
                 }
                 return v;
             };
@@ -1424,7 +1457,10 @@ int dls_conv_stem_bn_act_f32(const float *x, int64_t B, int32_t C, int32_t H, in
     a.co_tiles = Cout / kWaveTile;
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     DLS_REQUIRE(blocks <= INT32_MAX, DLS_EINVAL, "dls_conv_stem_bn_act_f32: %lld blocks", (long long)blocks);
-    if (C == 3 && KH == 3 && KW == 3)  // the CIFAR ResNet stem
+    if (DLS_STEM_WINDOW && C == 3 && KH == 3 && KW == 3 && stride == 1 && pad == 1 && W == 32 && H % 8 == 0)
+        hipLaunchKernelGGL((k_conv_stem<WPIX, 3, 3, true>), dim3((unsigned)blocks), dim3(64 * WPIX), 0,
+                           as_stream(stream), a, x);  // the CIFAR ResNet stem, window staged in LDS
+    else if (C == 3 && KH == 3 && KW == 3)
         hipLaunchKernelGGL((k_conv_stem<WPIX, 3, 3>), dim3((unsigned)blocks), dim3(64 * WPIX), 0,
                            as_stream(stream), a, x);
     else
