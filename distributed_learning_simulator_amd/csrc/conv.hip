@@ -40,8 +40,11 @@
 //                   halo buffers);
 //   k_conv3x3_halo  the same tiling register-staged (shapes whose halo tile the
 //                   pipeline's LDS budget does not fit; none of ResNet-18's);
-//   k_conv_bf16x3   anything else (stride 2, 1x1, sizes the halo tiling does
-//                   not fit): every (tap, chunk) gathers its B tile.
+//   k_conv3x3s2_phase  3x3 stride-2 convolutions as four stride-1 ones over
+//                   the input's row / column parity images, on the same
+//                   pipeline (each input pixel staged once per channel chunk);
+//   k_conv_bf16x3   anything else (1x1, sizes the tilings do not fit): every
+//                   (tap, chunk) gathers its B tile.
 // The epilogue goes through LDS: the raw tile is transposed to [pixel][channel]
 // and each thread applies the eval batch norm with the batch-norm library's
 // arithmetic (infer.hip, k_bn_act_exact: fma(w, (x - mean) * iv, b)), the
