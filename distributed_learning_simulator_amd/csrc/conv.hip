@@ -1289,6 +1289,7 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
     const int H = a.H, W = a.W;
     if (32 % W) return 0;  // a wave's two 32-pixel tiles share their columns
+    if ((int64_t)a.B * H * W >= (1ll << 28)) return 0;  // halo sources: input pixel * 8 + piece in 32 bits
     const int TR = H < BNP / W ? H : BNP / W;
     int TI = 1;
     if (TR == H) {
