@@ -108,6 +108,33 @@ def test_conv_bn_act_matches_fp64(shape):
     assert y.shape == ref.shape and torch.isfinite(y).all()
 
 
+def _fuzz_cases(n=24, seed=2026):
+    import random
+    rnd = random.Random(seed)
+    cases = []
+    while len(cases) < n:
+        cin = rnd.choice([32, 64, 96, 128, 256])
+        cout = rnd.choice([64, 128, 192, 256])
+        s = rnd.choice([1, 1, 2])
+        hw = rnd.choice([4, 8, 16, 32]) if s == 1 else rnd.choice([8, 16, 32])
+        h = hw if rnd.random() < 0.7 else hw // 2 if hw > 4 else hw
+        b = rnd.randint(1, 6)
+        if b * h * hw * max(cin, cout) > 2 ** 21:  # keep the fp64 reference quick
+            continue
+        cases.append((cin, cout, 3, s, h, hw, rnd.random() < 0.5, b))
+    return cases
+
+
+@pytest.mark.parametrize("shape", _fuzz_cases(), ids=lambda t: "c{}-{}s{}_{}x{}{}_b{}".format(
+    t[0], t[1], t[3], t[4], t[5], "_res" if t[6] else "", t[7]))
+def test_conv_bn_act_random_shapes_match_fp64(shape):
+    """A seeded sweep over the shapes the 3x3 kernels choose between (the LDS-DMA
+    pipeline's 4- / 8-wave and one- / two-halo-buffer forms, the stride-2 phase
+    pipeline, the register-staged fallbacks): odd channel-chunk counts, 64- and
+    128-multiple output channels, non-square images, partial tiles."""
+    test_conv_bn_act_matches_fp64(shape)
+
+
 def test_conv_bit_identical_on_repeat():
     """The same inputs -> the same bits: repeated launches, launches of other shapes
     in between, and fresh copies of the operands (other addresses)."""
