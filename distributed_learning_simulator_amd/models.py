@@ -99,9 +99,11 @@ class ResNet18(nn.Module):
 
     @torch.no_grad()
     def pack_split(self):
-        """The operands of forward_split: {id(conv): split weights} and {id(bn):
-        exact eval batch-norm consts} (recomputed per evaluation: the weights
-        change with the coalition)."""
+        """The operands of forward_split: {id(conv): split weights}, {id(bn):
+        exact eval batch-norm consts} and {id(linear): (weight, bias) copies}
+        (recomputed per evaluation: the weights change with the coalition).  The
+        forward reads nothing else of the module, so the module may be overwritten
+        once this returns while the forward is still queued on another stream."""
         from . import _native
         pk = {}
         for m in self.modules():
@@ -117,6 +119,9 @@ class ResNet18(nn.Module):
                 c = torch.empty(4 * m.num_features, device=m.running_mean.device)
                 _native.bn_fold_exact(m, c)
                 pk[id(m)] = c
+            elif isinstance(m, nn.Linear):
+                pk[id(m)] = (m.weight.detach().contiguous().clone(),
+                             None if m.bias is None else m.bias.detach().contiguous().clone())
         return pk
 
     def split_activation_bytes(self, H, W):
@@ -158,7 +163,8 @@ class ResNet18(nn.Module):
                 h = cba(out, blk.conv1, blk.bn1)
                 sc = cba(out, blk.shortcut[0], blk.shortcut[1], relu=False) if len(blk.shortcut) else out
                 out = cba(h, blk.conv2, blk.bn2, residual=sc)
-        return _native.pool_linear(out, self.linear.weight, self.linear.bias)
+        lw, lb = pk[id(self.linear)]
+        return _native.pool_linear(out, lw, lb)
 
     def forward_fused(self, x, fold):
         """forward() for utility evaluation on the GPU: NHWC or NCHW activations,

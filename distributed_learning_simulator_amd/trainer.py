@@ -234,12 +234,7 @@ class Inferencer:
             # budget: a 10k-image evaluation in one forward runs 3 % faster than in
             # 2,048-image ones and 4 % faster than in 1,000-image ones
             # (profiles/r05_conv_probe.txt r05bs3)
-            bs = self.split_batch(X.shape[0])
-            pk = self.model.pack_split()
-            for i in range(0, X.shape[0], bs):
-                xb = X[i:i + bs].to(self.device, torch.float32, non_blocking=True)
-                yb = y[i:i + bs].to(self.device, non_blocking=True)
-                yield split(xb.contiguous(), pk), yb
+            yield from self._split_batches(X, y, split, self.model.pack_split())
             return
         fmt = self._memory_format()
         if X.dim() == 4 and torch.device(self.device).type == "cuda":
@@ -258,6 +253,13 @@ class Inferencer:
                 xb = xb.contiguous(memory_format=fmt)
             yield (fused(xb, fold) if fused is not None else self.model(xb)), yb
 
+    def _split_batches(self, X, y, split, pk):
+        bs = self.split_batch(X.shape[0])
+        for i in range(0, X.shape[0], bs):
+            xb = X[i:i + bs].to(self.device, torch.float32, non_blocking=True)
+            yb = y[i:i + bs].to(self.device, non_blocking=True)
+            yield split(xb.contiguous(), pk), yb
+
     @torch.no_grad()
     def logits(self):
         """The logits ``inference()`` scores, concatenated over the dataset."""
@@ -265,11 +267,40 @@ class Inferencer:
             return torch.cat([out for out, _ in self._batches()])
 
     @torch.no_grad()
-    def correct_async(self):
+    def correct_async(self, stream=None):
         """The top-1 correct count over the dataset as a device int64 tensor, with
         no host synchronisation: ``inference()``'s accuracy is ``int(count) / n``.
         The Shapley servers queue a batch of coalitions' evaluations this way and
-        read all counts with one synchronisation."""
+        read all counts with one synchronisation.
+
+        ``stream``: run the forward there (the library's convolutions only; else
+        it runs on the current stream).  The model's operands are packed on the
+        current stream first (ResNet18.pack_split copies everything the forward
+        reads), so the caller may load the next model as soon as this returns
+        and queue that model's forward on another stream: two forwards in flight
+        fill each other's layer ramps and memory phases.  The count is ready on
+        ``stream``; make the current stream wait for it before reading it.  The
+        same bits on any stream (every kernel's arithmetic is fixed by the
+        shape)."""
+        split = self._split_forward() if stream is not None else None
+        if split is not None:
+            cur = torch.cuda.current_stream(self.device)
+            X, y = self._resident_dataset()
+            self.model.eval()
+            pk = self.model.pack_split()
+            stream.wait_stream(cur)
+            for t in (X, y):
+                if t.is_cuda:
+                    t.record_stream(stream)
+            with torch.cuda.stream(stream):
+                correct = torch.zeros((), dtype=torch.int64, device=self.device)
+                for out, yb in self._split_batches(X, y, split, pk):
+                    correct += (out.argmax(1) == yb).sum()
+            for t in pk.values():  # freed by the host now, read by `stream` later
+                for u in (t if isinstance(t, tuple) else (t,)):
+                    if u is not None:
+                        u.record_stream(stream)
+            return correct
         with self._flags():
             correct = torch.zeros((), dtype=torch.int64, device=self.device)
             for out, yb in self._batches():

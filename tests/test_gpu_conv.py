@@ -347,3 +347,38 @@ def test_bf16x3_utilities_equal_fp32_utilities_at_config5_scale():
           f"flipped top-1 predictions {flips} of 160,000 (near-ties {near_flips})")
     assert flips == near_flips
     assert max(diffs) <= 3e-4 + 1e-12
+
+
+def test_queued_evaluations_on_several_streams_equal_one_stream():
+    """ShapleyValueServer.evaluate_subsets queues each coalition's forward on one of
+    eval_streams HIP streams (two forwards in flight): the utilities are the same
+    floats as with one stream and as get_metric's synchronous inference(), the
+    model may be overwritten while an earlier forward is still queued (pack_split
+    copies every operand, the linear layer included), and a dataset read on
+    several streams is not released early."""
+    from distributed_learning_simulator_amd.model_util import ModelUtil
+    from distributed_learning_simulator_amd.models import ResNet18, synthetic_classification
+    from distributed_learning_simulator_amd.servers.shapley_value_server import ShapleyValueServer
+    from distributed_learning_simulator_amd.trainer import Inferencer
+    torch.manual_seed(31)
+    base = ModelUtil(_resnet(13)).get_parameter_dict()
+    X, y = synthetic_classification(3000, (3, 32, 32), seed=14)
+    tester = Inferencer(ResNet18().to(dev), (X, y), batch_size=1000, device=dev)
+    server = ShapleyValueServer(tester=tester, worker_number=6, synchronous=True, device=dev,
+                                subset_batch=4)
+    g = torch.Generator(device=dev).manual_seed(31)
+    for wid in range(6):
+        server.parameters[wid] = (50 + 7 * wid, {
+            k: v + torch.randn(v.shape, generator=g, device=dev) * 0.05 for k, v in base.items()})
+    server._set_prev_model(base)
+    coal = [(0,), (1, 2), (), (0, 3, 5), (4,), (1, 2, 3, 4, 5), (2, 5), (0, 1, 2, 3, 4, 5), (3,)]
+    out = {}
+    for ns in (1, 2, 3):
+        server.eval_streams = ns
+        out[ns] = server.evaluate_subsets(coal)
+    assert server._streams is not None and len(server._streams) == 3
+    assert out[1] == out[2] == out[3]
+    sync = [float(server.get_metric(server.get_subset_model(list(c)) if c else server.prev_model))
+            for c in coal]
+    assert out[2] == sync
+    assert len(set(out[2])) > 2  # the coalitions' models differ
