@@ -32,6 +32,9 @@
 // output tile = 2 x 2 MFMA tiles; operands are staged in chunks of 32 channels
 // through LDS (register staging, rows padded by 16 B: conflict-free
 // ds_read_b128 fragments).  Kernels:
+//   k_conv3x3_pipe16  3x3 stride-1 convolutions (the default): k_conv3x3_pipe's
+//                   pipeline on v_mfma_f32_16x16x32_bf16 (4 x 4 tiles of 16 x 16
+//                   per wave; -2 % per forward, profiles/r06_conv_mf16_ab.txt);
 //   k_conv3x3_pipe  3x3 stride-1 convolutions: the block's pixels are whole
 //                   output rows, so its input is ONE halo tile staged once per
 //                   channel chunk and read by all 9 taps at shifted rows; every
@@ -62,6 +65,9 @@
 #endif
 #ifndef DLS_STEM_WINDOW  // probe knob: 0 = the stem's 27 terms gathered from global memory
 #define DLS_STEM_WINDOW 1
+#endif
+#ifndef DLS_CONV_MF16  // probe knob: 0 = the 3x3 stride-1 pipeline on 32x32x16 MFMAs (k_conv3x3_pipe)
+#define DLS_CONV_MF16 1
 #endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
@@ -123,6 +129,7 @@ constexpr int kBK = 32;        // channels per staged chunk
 constexpr int kRowB = 4 * kBK + 16;  // LDS row: kBK hi, kBK lo (bf16), 16 B pad
 
 typedef f32x16 WaveAcc[2][2];
+typedef f32x4 WaveAcc16[4][4];  // the same 64 x 64 tile as 4 x 4 tiles of 16 x 16
 
 // One staged chunk (kBK channels) into the wave's 2 x 2 tiles: A rows from `arow`
 // (this lane's row r of the wave's first 32-channel tile; the second at +32
@@ -192,8 +199,43 @@ __device__ __forceinline__ void zero_acc(WaveAcc &acc) {
 // 32-channel tile i of every wave per pass (half the LDS; the same arithmetic
 // per element): pass p's local channel lc is channel (lc / 32) * 64 + 32 p +
 // lc % 32 of the block.
-template <int BMC, int BNP, int NT, int NPASS = 1>
-__device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, const ConvArgs &a,
+// The raw tile of a wave into the epilogue's [pixel][channel] fp32 image (pass p)
+template <int NPASS, int EROW>
+__device__ __forceinline__ void acc_to_lds(const WaveAcc &acc, uint8_t *smem, int wc, int wp, int lane, int p) {
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (NPASS == 2 && i != p) continue;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int pl = wp * kWaveTile + 32 * j + r;
+                const int cl = NPASS == 1 ? wc * kWaveTile + 32 * i + 8 * g + 4 * h : wc * 32 + 8 * g + 4 * h;
+                *reinterpret_cast<f32x4 *>(smem + pl * EROW + cl * 4) =
+                    f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+            }
+        }
+}
+
+// 16x16x32 tiles: lane (r = l & 15, q = l >> 4) of tile (i, j) holds channels
+// 16 i + 4 q + e of pixel 16 j + r
+template <int NPASS, int EROW>
+__device__ __forceinline__ void acc_to_lds(const WaveAcc16 &acc, uint8_t *smem, int wc, int wp, int lane, int) {
+    static_assert(NPASS == 1, "one epilogue pass");
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pl = wp * kWaveTile + 16 * j + r;
+            const int cl = wc * kWaveTile + 16 * i + 4 * q;
+            *reinterpret_cast<f32x4 *>(smem + pl * EROW + cl * 4) = acc[i][j];
+        }
+}
+
+template <int BMC, int BNP, int NT, int NPASS = 1, class Acc = WaveAcc>
+__device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, const ConvArgs &a,
                                              int co0, int pix0, int wc, int wp, int tid) {
     static_assert(NPASS == 1 || NPASS == 2, "epilogue passes");
     constexpr int SLAB = BMC / NPASS;  // channels per pass
@@ -201,7 +243,7 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
     constexpr int GPP = SLAB / 8;      // 8-channel groups per pixel
     constexpr int NPC = BNP * GPP / NT;
     static_assert(NT % GPP == 0 && (BNP * GPP) % NT == 0, "epilogue shape");
-    const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int lane = tid & 63;
     const int lc = 8 * (tid % GPP);  // a thread's channel group is fixed per pass
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
@@ -220,19 +262,7 @@ __device__ __forceinline__ void epilogue_lds(const WaveAcc &acc, uint8_t *smem, 
             }
         }
         if (p > 0) __syncthreads();  // the previous pass's reads are done
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if (NPASS == 2 && i != p) continue;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int pl = wp * kWaveTile + 32 * j + r;
-                    const int cl = NPASS == 1 ? wc * kWaveTile + 32 * i + 8 * g + 4 * h : wc * 32 + 8 * g + 4 * h;
-                    *reinterpret_cast<f32x4 *>(smem + pl * EROW + cl * 4) =
-                        f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                }
-            }
+        acc_to_lds<NPASS, EROW>(acc, smem, wc, wp, lane, p);
         __syncthreads();
         // the 8 channels' batch-norm constants as element pairs: 8 vector loads
         f32x2 m2[4], iv2[4], wv2[4], bv2[4];
@@ -794,6 +824,211 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     epilogue_lds<BMC, BNP, NT>(acc, smem, a, co0, pix0, wc, wp, tid);
 }
 
+// k_conv3x3_pipe on v_mfma_f32_16x16x32_bf16: a wave's 64 x 64 tile as 4 x 4
+// tiles of 16 x 16, one MFMA per (tile, product) covering the whole 32-channel
+// step (the 16 A / B fragment reads per step are k_conv3x3_pipe's 16).  Under
+// load the chip holds a higher clock on this shape than on 32x32x16
+// (MI355X_MICROARCH.md, DVFS give-back item 7).  The 16-B pieces are swizzled
+// by row & 7 (a 16-row fragment read at any row offset is conflict-free; the
+// 32-row form's (row >> 1) & 7 is 2-way at odd offsets).  A step's fragments are
+// read whole a step ahead (two sets in registers), the next step's during this
+// step's 48 MFMAs.  Reduction order per output: chunks, taps, then per step the
+// products lo*hi, hi*lo, hi*hi over the 32 channels inside the MFMA — not
+// k_conv3x3_pipe's bits.
+// A step's fragments in two parts: A (all four channel tiles) with pixel tiles
+// 0-1, and pixel tiles 2-3 (read during the MFMAs of the first part)
+struct Frag16A {
+    bf16x8 ah[4], al[4], bh[2], bl[2];
+};
+struct Frag16B {
+    bf16x8 bh[2], bl[2];
+};
+
+// the MFMAs of pixel tiles jb, jb + 1 (products lo*hi, hi*lo, hi*hi)
+__device__ __forceinline__ void mfma_half16(WaveAcc16 &acc, const Frag16A &fa, const bf16x8 (&bh)[2],
+                                            const bf16x8 (&bl)[2], int jb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            f32x4 &c = acc[i][jb + j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.al[i], bh[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.ah[i], bl[j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.ah[i], bh[j], c, 0, 0, 0);
+        }
+}
+
+template <int WCO, int WPIX, int NHI, int NHB = 2, int OCC = 1>
+__global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe16(ConvArgs a) {
+    constexpr int NW = WCO * WPIX, NT = 64 * NW;
+    constexpr int BMC = kWaveTile * WCO, BNP = kWaveTile * WPIX;
+    constexpr int RB = 128;
+    constexpr int HROWS = 8 * NW * NHI;
+    constexpr int HB = HROWS * RB, AB = BMC * RB;
+    constexpr int NAI = BMC / (8 * NW);
+    constexpr int STAGE = NHB * HB + 3 * AB + 2 * RB;
+    constexpr int EPI = BNP * (4 * BMC + 16);
+    static_assert(BMC % (8 * NW) == 0 && NAI >= 1, "weight rows per wave");
+    static_assert(NHB == 1 || NHI <= 7, "the halo pieces go out in taps 0..6");
+    static_assert(NHB == 1 || NHB == 2, "halo buffers");
+    static_assert(kBK == 32, "128-byte rows");
+    __shared__ __attribute__((aligned(16))) uint8_t smem[STAGE > EPI ? STAGE : EPI];
+    uint8_t *const hbuf0 = smem;
+    uint8_t *const abuf0 = smem + NHB * HB;
+    uint8_t *const zrow = abuf0 + 3 * AB;
+
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wc = wv / WPIX, wp = wv % WPIX;
+    int co_t, pt;
+    tile_of_block(a.co_tiles, co_t, pt);
+    const int co0 = co_t * BMC;
+    const int pix0 = pt * BNP;
+    const int W = a.W, H = a.H, TR = a.TR;
+    const int hrows_img = (TR + 2) * W;
+    int b0, y0;
+    if (TR == H) {
+        b0 = pt * a.TI;
+        y0 = 0;
+    } else {
+        const int tpi = H / TR;
+        b0 = pt / tpi;
+        y0 = (pt - b0 * tpi) * TR;
+    }
+
+    // DMA sources as k_conv3x3_pipe's, the piece swizzled by the row's key & 7
+    const int sl = lane & 7, lr = lane >> 3;
+    int hsrc[NHI];
+#pragma unroll
+    for (int u = 0; u < NHI; ++u) {
+        const int hr = 8 * (u * NW + wv) + lr;
+        int pix = -1, s = 0;
+        if (hr < a.NH) {
+            const int ti = hr / hrows_img, rem = hr - ti * hrows_img;
+            const int ry = rem / W, rx = rem - ry * W;
+            s = hr - 2 * W * ti;
+            const int b = b0 + ti, iy = y0 - 1 + ry;
+            if (b < a.B && (unsigned)iy < (unsigned)H) pix = (b * H + iy) * W + rx;
+        }
+        hsrc[u] = pix >= 0 ? pix * 8 + (sl ^ (s & 7)) : -1;
+    }
+    const uint16_t *zero = reinterpret_cast<const uint16_t *>(kZeroPiece);
+    asm volatile("" : "+s"(zero));
+    const uint16_t *asrc[NAI];
+#pragma unroll
+    for (int u = 0; u < NAI; ++u) {
+        const int row = 8 * (wv * NAI + u) + lr;
+        const int p = sl ^ (row & 7);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
+    }
+    auto issue_weights = [&](int step, int slot) {
+        const int cc = step / 9, tap = step - 9 * cc;
+        int Cv = a.C;  // opaque per step: no per-tap source addresses hoisted out of the loop
+        asm volatile("" : "+s"(Cv));
+        const int kc = tap * Cv + cc * kBK;
+        uint8_t *dst = abuf0 + (slot % 3) * AB;
+#pragma unroll
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
+    };
+    auto issue_halo = [&](int u, int cc) {
+        const int v = hsrc[u], p = v & 7;
+        const uint16_t *src =
+            v >= 0 ? a.x + (int64_t)(v >> 3) * (2 * a.C) + ((p & 4) ? a.C : 0) + 8 * (p & 3) + cc * kBK : zero;
+        glds16(src, hbuf0 + (NHB == 2 ? (cc & 1) * HB : 0) + (u * NW + wv) * 8 * RB);
+    };
+
+    // lane (r, q): A rows wc*64 + 16 i + r, pieces q (hi) and 4 + q (lo); B rows of
+    // the pixels wp*64 + 16 j + r
+    const int r = lane & 15, q = lane >> 4;
+    const int arow = (wc * kWaveTile + r) * RB;
+    const int qa = 16 * (q ^ (r & 7)), qla = 16 * ((4 + q) ^ (r & 7));  // (wc*64 + 16 i + r) & 7 = r & 7
+    int hb[4], ox[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int pl = wp * kWaveTile + 16 * j + r;
+        const int tw = TR * W;
+        const int ti = pl / tw, rem = pl - ti * tw;
+        const int oy = rem / W;
+        ox[j] = rem - oy * W;
+        hb[j] = ti * hrows_img + oy * W + ox[j];  // its halo row under tap (0, 1)
+    }
+    const int pl0 = wp * kWaveTile + r;
+    // B fragments of pixel tiles jb, jb + 1 at a step's tap
+    auto fragb = [&](bf16x8 (&bh)[2], bf16x8 (&bl)[2], int step, int tap, int jb) {
+        const uint8_t *hbb = hbuf0 + (NHB == 2 ? ((step / 9) & 1) * HB : 0);
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        // W made opaque per read: the rows are recomputed each step (a few adds)
+        // instead of 9 taps x 4 tiles of addresses hoisted out of the chunk loop
+        int Wv = W;
+        asm volatile("" : "+s"(Wv));
+        const int sh = ky * Wv + kx - 1;
+        const int key = (pl0 + sh) & 7;  // + 16 j: the same key
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool in = (unsigned)(ox[jb + j] + kx - 1) < (unsigned)Wv;
+            const uint8_t *row = in ? hbb + (hb[jb + j] + sh) * RB : zrow + ((pl0 + sh) & 1) * RB;
+            bh[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * (q ^ key));
+            bl[j] = *reinterpret_cast<const bf16x8 *>(row + 16 * ((4 + q) ^ key));
+        }
+    };
+    auto fraga = [&](Frag16A &f, int step, int tap) {
+        const uint8_t *ab = abuf0 + (step % 3) * AB + arow;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f.ah[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 16 * RB + qa);
+            f.al[i] = *reinterpret_cast<const bf16x8 *>(ab + i * 16 * RB + qla);
+        }
+        fragb(f.bh, f.bl, step, tap, 0);
+    };
+
+    WaveAcc16 acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nc = a.C / kBK, T = 9 * nc;
+    if (tid < 2 * RB / 16) *reinterpret_cast<u32x4 *>(zrow + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < NHI; ++u) issue_halo(u, 0);
+    issue_weights(0, 0);
+    issue_weights(T > 1 ? 1 : 0, 1);
+    retire_and_barrier<NW>(false);
+    Frag16A fa;
+    Frag16B fb;
+    fraga(fa, 0, 0);
+    for (int cc = 0; cc < nc; ++cc) {
+        const bool more = cc + 1 < nc;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int t = 9 * cc + tap;
+            const bool piece = NHB == 2 && more && tap < NHI;
+            issue_weights(t + 2 < T ? t + 2 : T - 1, t + 2);
+            if (piece) issue_halo(tap, cc + 1);
+            const bool reload = NHB == 1 && tap == 8 && more;  // the next chunk's halo is not in yet
+            __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // A and pixel tiles 0-1 of this step
+            fragb(fb.bh, fb.bl, t, tap, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_half16(acc, fa, fa.bh, fa.bl, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // pixel tiles 2-3
+            const Frag16A cur = fa;
+            if (!reload) fraga(fa, t + 1, tap == 8 ? 0 : tap + 1);  // past the last step: stale LDS, unused
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_half16(acc, cur, fb.bh, fb.bl, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            retire_and_barrier<NW>(piece);
+            if (reload) {  // every wave is past its reads of this chunk's halo
+#pragma unroll
+                for (int u = 0; u < NHI; ++u) issue_halo(u, cc + 1);
+                retire_and_barrier<NW>(false);
+                fraga(fa, t + 1, 0);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last fragment read
+    epilogue_lds<BMC, BNP, NT, 1, WaveAcc16>(acc, smem, a, co0, pix0, wc, wp, tid);
+}
+
 // --------------------------------------------- 3x3, stride 2, pad 1: phases
 // A stride-2 3x3 convolution is four stride-1 ones over the input's row / column
 // parity images P_ab(q, r) = x(2q + a, 2r + b), each Ho x Wo: tap (ky, kx) reads
@@ -1283,7 +1518,8 @@ int try_launch_phase(ConvArgs a, hipStream_t st, int &rc) {
     return 1;
 }
 
-// The LDS-DMA pipeline (k_conv3x3_pipe) when the halo tile fits NHI DMAs per wave
+// The LDS-DMA pipeline (k_conv3x3_pipe, or k_conv3x3_pipe16 with DLS_CONV_MF16)
+// when the halo tile fits NHI DMAs per wave
 template <int WCO, int WPIX, int NHI, int NHB = 2, int OCC = 1>
 int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     constexpr int BNP = kWaveTile * WPIX;
@@ -1309,8 +1545,12 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     a.co_tiles = a.Cout / (kWaveTile * WCO);
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     if (blocks > INT32_MAX) return 0;
-    hipLaunchKernelGGL((k_conv3x3_pipe<WCO, WPIX, NHI, NHB, OCC>), dim3((unsigned)blocks), dim3(64 * WCO * WPIX), 0,
-                       st, a);
+    if (DLS_CONV_MF16)
+        hipLaunchKernelGGL((k_conv3x3_pipe16<WCO, WPIX, NHI, NHB, OCC>), dim3((unsigned)blocks),
+                           dim3(64 * WCO * WPIX), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_conv3x3_pipe<WCO, WPIX, NHI, NHB, OCC>), dim3((unsigned)blocks),
+                           dim3(64 * WCO * WPIX), 0, st, a);
     rc = check_launch("dls_conv_bn_act_split");
     return 1;
 }
