@@ -712,7 +712,7 @@ def conv_eval_roofline(tester, reps=3):
             ts.append(e0.elapsed_time(e1))
     ms = sorted(ts)[len(ts) // 2]
     ach = 6 * issued * n / (ms / 1e3) / 1e12
-    return {"kernel": "dls_conv_bn_act_split (k_conv3x3_pipe, k_conv3x3s2_phase, k_conv_bf16x3, k_conv_stem) + pool_linear",
+    return {"kernel": "dls_conv_bn_act_split (k_conv3x3_pipe16, k_conv3x3s2_phase, k_conv_bf16x3, k_conv_stem) + pool_linear",
             "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s (bf16 MFMA issued)", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
             "traffic": None, "ms_per_forward_of_all_images": round(ms, 3),
