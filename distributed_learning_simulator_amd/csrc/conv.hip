@@ -69,6 +69,9 @@
 #ifndef DLS_CONV_MF16  // probe knob: 0 = the 3x3 stride-1 pipeline on 32x32x16 MFMAs (k_conv3x3_pipe)
 #define DLS_CONV_MF16 1
 #endif
+#ifndef DLS_STEM_TILES  // probe knob: pixel tiles per block of the CIFAR stem (k_conv_stem, XT)
+#define DLS_STEM_TILES 4
+#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -1235,7 +1238,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs
 // staged in LDS by one 16-B load per thread and the 27 terms gathered from there,
 // instead of 27 scalar loads per thread from global memory; the same values.
 constexpr int kStemWinRow = 40;  // floats per window row: image column ix at ix + 4
-template <int WPIX, int CIN = 0, int KHW = 0, bool XT = false>
+// NTL > 1 (XT): a block walks NTL consecutive pixel tiles with its A fragments
+// loaded once, the next tile's input window loaded into registers while this
+// tile is gathered, multiplied and stored; the same arithmetic per tile.
+template <int WPIX, int CIN = 0, int KHW = 0, bool XT = false, int NTL = 1>
 __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float *__restrict__ x) {
     constexpr int NT = 64 * WPIX, BNP = kWaveTile * WPIX;
     constexpr int STAGE = BNP * kRowB;
@@ -1243,6 +1249,7 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
     constexpr int WIN = XT ? 3 * 10 * kStemWinRow * 4 : 0;
     static_assert(NT == BNP, "one pixel row per thread");
     static_assert(!XT || (CIN == 3 && KHW == 3 && BNP == 256), "the staged window's shape");
+    static_assert(NTL == 1 || XT, "tile walks: the staged-window form");
     __shared__ __attribute__((aligned(16))) uint8_t smem[(STAGE > EPI ? STAGE : EPI) + WIN];
     uint8_t *Bs = smem;
     float *win = reinterpret_cast<float *>(smem + (STAGE > EPI ? STAGE : EPI));
@@ -1251,25 +1258,20 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
     int co_t, pix_t;
     tile_of_block(a.co_tiles, co_t, pix_t);
     const int co0 = co_t * kWaveTile;
-    const int pix0 = pix_t * BNP;
-    if constexpr (XT) {  // rows oy0 - 1 .. oy0 + 8 of the tile's image, 8 columns x 4 per thread
-        const int b = pix0 / (a.H * 32), oy0 = (pix0 - b * a.H * 32) / 32;
+    // the window rows oy0 - 1 .. oy0 + 8 of a tile's image, 8 columns x 4 per thread
+    auto load_window = [&](int p0) {
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int b = p0 / (a.H * 32), oy0 = (p0 - b * a.H * 32) / 32;
         if (tid < 240) {
             const int ci = tid / 80, rem = tid - ci * 80, wy = rem / 8, c4 = rem - wy * 8;
             const int iy = oy0 - 1 + wy;
-            f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
             if (b < a.B && (unsigned)iy < (unsigned)a.H)
                 v = *reinterpret_cast<const f32x4 *>(x + (((int64_t)b * 3 + ci) * a.H + iy) * 32 + 4 * c4);
-            *reinterpret_cast<f32x4 *>(win + (ci * 10 + wy) * kStemWinRow + 4 + 4 * c4) = v;
-        } else if (tid < 240 + 15) {  // the padding columns (image columns -1 and 32) of 30 rows
-            const int q = tid - 240;
-            win[(2 * q) * kStemWinRow + 3] = 0.f;
-            win[(2 * q) * kStemWinRow + 36] = 0.f;
-            win[(2 * q + 1) * kStemWinRow + 3] = 0.f;
-            win[(2 * q + 1) * kStemWinRow + 36] = 0.f;
         }
-        __syncthreads();
-    }
+        return v;
+    };
+    f32x4 wnext = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (XT) wnext = load_window(pix_t * NTL * BNP);
     // A fragments of both k-steps (in flight during the gather): channel tile i,
     // lane row co0 + 32 i + r, k = 16 s + 8 h .. + 7 (hi), + K (lo)
     Frag f[kBK / 16];
@@ -1281,6 +1283,24 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
             f[s].ah[i] = *reinterpret_cast<const bf16x8 *>(wr);
             f[s].al[i] = *reinterpret_cast<const bf16x8 *>(wr + a.K);
         }
+    for (int tl = 0; tl < NTL; ++tl) {
+    const int pix0 = (pix_t * NTL + tl) * BNP;
+    if (pix0 >= a.M) break;  // block-uniform
+    if constexpr (XT) {
+        if (tl > 0) __syncthreads();  // the previous tile's epilogue is done with the LDS
+        if (tid < 240) {
+            const int ci = tid / 80, rem = tid - ci * 80, wy = rem / 8, c4 = rem - wy * 8;
+            *reinterpret_cast<f32x4 *>(win + (ci * 10 + wy) * kStemWinRow + 4 + 4 * c4) = wnext;
+        } else if (tid < 240 + 15) {  // the padding columns (image columns -1 and 32) of 30 rows
+            const int q = tid - 240;
+            win[(2 * q) * kStemWinRow + 3] = 0.f;
+            win[(2 * q) * kStemWinRow + 36] = 0.f;
+            win[(2 * q + 1) * kStemWinRow + 3] = 0.f;
+            win[(2 * q + 1) * kStemWinRow + 36] = 0.f;
+        }
+        __syncthreads();
+        if (tl + 1 < NTL && pix0 + BNP < a.M) wnext = load_window(pix0 + BNP);  // in flight until the next tile
+    }
     // this thread's pixel: gather, split, one LDS row
     {
         const int p = pix0 + tid;
@@ -1334,6 +1354,7 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
     }
     __syncthreads();  // the epilogue reuses the operands' LDS
     epilogue_lds<kWaveTile, BNP, NT, 2>(acc, smem, a, co0, pix0, 0, wp, tid);
+    }
 }
 
 // fp32 NCHW image batch -> split NHWC with Cp >= C channels (zeros beyond C)
@@ -1701,9 +1722,13 @@ int dls_conv_stem_bn_act_f32(const float *x, int64_t B, int32_t C, int32_t H, in
     a.co_tiles = Cout / kWaveTile;
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
     DLS_REQUIRE(blocks <= INT32_MAX, DLS_EINVAL, "dls_conv_stem_bn_act_f32: %lld blocks", (long long)blocks);
-    if (DLS_STEM_WINDOW && C == 3 && KH == 3 && KW == 3 && stride == 1 && pad == 1 && W == 32 && H % 8 == 0)
-        hipLaunchKernelGGL((k_conv_stem<WPIX, 3, 3, true>), dim3((unsigned)blocks), dim3(64 * WPIX), 0,
-                           as_stream(stream), a, x);  // the CIFAR ResNet stem, window staged in LDS
+    if (DLS_STEM_WINDOW && C == 3 && KH == 3 && KW == 3 && stride == 1 && pad == 1 && W == 32 && H % 8 == 0) {
+        // the CIFAR ResNet stem, window staged in LDS, DLS_STEM_TILES pixel tiles per block
+        constexpr int NTL = DLS_STEM_TILES;
+        const int64_t walks = (int64_t)((a.pix_tiles + NTL - 1) / NTL) * a.co_tiles;
+        hipLaunchKernelGGL((k_conv_stem<WPIX, 3, 3, true, NTL>), dim3((unsigned)walks), dim3(64 * WPIX), 0,
+                           as_stream(stream), a, x);
+    }
     else if (C == 3 && KH == 3 && KW == 3)
         hipLaunchKernelGGL((k_conv_stem<WPIX, 3, 3>), dim3((unsigned)blocks), dim3(64 * WPIX), 0,
                            as_stream(stream), a, x);
