@@ -375,7 +375,7 @@ def bn_act_exact(x, consts, residual=None, relu=True, out=None, inplace=False, s
 # ------------------------------------------------ deterministic convolutions
 # "split" tensors (csrc/conv.hip): an fp32 value as a bf16 pair (hi, lo), stored
 # as int16 — activations [B, H, W, 2C] (per pixel C hi then C lo), weights
-# [Cout, 2K] (K hi then K lo, k = (ky*KW + kx)*Cp + ci).
+# [Cout, 2K] (chunk-major: per 32-wide chunk of k, 32 hi then 32 lo; k = (ky*KW + kx)*Cp + ci).
 
 def _check_same_device(fn, x, **others):
     for name, t in others.items():

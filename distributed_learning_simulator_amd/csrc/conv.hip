@@ -23,8 +23,11 @@
 // Layouts (HBM):
 //   activations  "split NHWC": uint16 [B][H][W][2C], per pixel C bf16 hi then C
 //                bf16 lo (4 B per element, the size of the fp32 tensor);
-//   weights      uint16 [Cout][2K], per output channel K hi then K lo,
-//                k = (ky * KW + kx) * C + ci (C = the input's padded channels).
+//   weights      uint16 [Cout][K / 32][64], chunk-major: per output channel and
+//                32-wide chunk of k, 32 hi then 32 lo, k = (ky * KW + kx) * C + ci
+//                (C = the input's padded channels), so a step's 32-channel row
+//                piece is one 128-B line (K hi then K lo made it two half lines:
+//                -1.8 % per forward, profiles/r06_conv_wchunk_ab.txt).
 // Implicit GEMM, D[co][pixel] = sum_k W[co][k] X[k][pixel]: A = weights (rows =
 // output channels), B = the input pixels' channel runs under a tap (zero outside
 // the image), so a lane's 16-element MFMA fragment is one 16-B piece of a
@@ -72,6 +75,9 @@
 #ifndef DLS_STEM_TILES  // probe knob: pixel tiles per block of the CIFAR stem (k_conv_stem, XT)
 #define DLS_STEM_TILES 4
 #endif
+#ifndef DLS_W_CHUNKED  // probe knob: 0 = split weights [Cout][K hi | K lo] (rounds 5-6); 1 = chunk-major (the ABI's)
+#define DLS_W_CHUNKED 1
+#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -118,7 +124,7 @@ __device__ __forceinline__ void split2x2(float a, float b, uint32_t &hi2, uint32
 
 struct ConvArgs {
     const uint16_t *x;      // split NHWC input [B][H][W][2C]
-    const uint16_t *w;      // split weights [Cout][2K]
+    const uint16_t *w;      // split weights [Cout][K / 32][32 hi | 32 lo]
     const float *consts;    // eval batch norm [mean | iv | w | b] x Cout, or null
     const uint16_t *res;    // split residual [B][Ho][Wo][2 Cout], or null
     uint16_t *y;            // split output [B][Ho][Wo][2 Cout]
@@ -130,6 +136,14 @@ struct ConvArgs {
 constexpr int kWaveTile = 64;  // a wave's output tile: 64 channels x 64 pixels
 constexpr int kBK = 32;        // channels per staged chunk
 constexpr int kRowB = 4 * kBK + 16;  // LDS row: kBK hi, kBK lo (bf16), 16 B pad
+
+// Offset (uint16 elements, within an output channel's 2K) of the 8 weights
+// k0 .. k0 + 7 (k0 a multiple of 8) of chunk-relative piece `part` (0..3 hi,
+// 4..7 lo) of the chunk starting at kc (a multiple of kBK)
+__device__ __forceinline__ int woff(int K, int kc, int part) {
+    if (DLS_W_CHUNKED) return 2 * kc + 8 * part;
+    return part < 4 ? kc + 8 * part : K + kc + 8 * (part - 4);
+}
 
 typedef f32x16 WaveAcc[2][2];
 typedef f32x4 WaveAcc16[4][4];  // the same 64 x 64 tile as 4 x 4 tiles of 16 x 16
@@ -397,7 +411,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
         const int tap = c / cchunks, ci0 = (c - tap * cchunks) * kBK;
         const int ky = tap / a.KW, kx = tap - ky * a.KW;
         const int kc = tap * a.C + ci0;
-        const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
+        const int wo = woff(a.K, kc, part);
 #pragma unroll
         for (int u = 0; u < NA; ++u) ra[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
         const int xo = part < HP ? ci0 + part * 8 : a.C + ci0 + (part - HP) * 8;
@@ -548,7 +562,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     };
     auto aload = [&](int cc, int tap) {
         const int kc = tap * a.C + cc * BK;
-        const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
+        const int wo = woff(a.K, kc, part);
 #pragma unroll
         for (int u = 0; u < NA; ++u) areg[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
     };
@@ -721,14 +735,14 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     for (int u = 0; u < NAI; ++u) {
         const int row = 8 * (wv * NAI + u) + lr;
         const int p = sl ^ ((row >> 1) & 7);
-        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + woff(a.K, 0, p);
     }
     auto issue_weights = [&](int step, int slot) {  // step's weights into ring slot slot % 3
         const int cc = step / 9, tap = step - 9 * cc;
         const int kc = tap * a.C + cc * kBK;
         uint8_t *dst = abuf0 + (slot % 3) * AB;
 #pragma unroll
-        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + (DLS_W_CHUNKED ? 2 * kc : kc), dst + (wv * NAI + u) * 8 * RB);
     };
     auto issue_halo = [&](int u, int cc) {
         const int v = hsrc[u], p = v & 7;
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe16(ConvArg
     for (int u = 0; u < NAI; ++u) {
         const int row = 8 * (wv * NAI + u) + lr;
         const int p = sl ^ (row & 7);
-        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + woff(a.K, 0, p);
     }
     auto issue_weights = [&](int step, int slot) {
         const int cc = step / 9, tap = step - 9 * cc;
@@ -930,7 +944,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe16(ConvArg
         const int kc = tap * Cv + cc * kBK;
         uint8_t *dst = abuf0 + (slot % 3) * AB;
 #pragma unroll
-        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + (DLS_W_CHUNKED ? 2 * kc : kc), dst + (wv * NAI + u) * 8 * RB);
     };
     auto issue_halo = [&](int u, int cc) {
         const int v = hsrc[u], p = v & 7;
@@ -1111,14 +1125,14 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs
     for (int u = 0; u < NAI; ++u) {
         const int row = 8 * (wv * NAI + u) + lr;
         const int p = sl ^ ((row >> 1) & 7);
-        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + woff(a.K, 0, p);
     }
     auto issue_weights = [&](int step, int slot) {
         const int cc = step / 9, tap = kPhaseTap[step - 9 * cc];
         const int kc = tap * a.C + cc * kBK;
         uint8_t *dst = abuf0 + (slot % 3) * AB;
 #pragma unroll
-        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + (DLS_W_CHUNKED ? 2 * kc : kc), dst + (wv * NAI + u) * 8 * RB);
     };
     // phase g = 4 cc + p (p: 0 = (1,1), 1 = (1,0), 2 = (0,1), 3 = (0,0)) into buffer g & 1
     auto issue_halo = [&](int g) {
@@ -1372,7 +1386,7 @@ __global__ __launch_bounds__(256) void k_pack_input(const float *__restrict__ x,
     y[pix * 2 * Cp + Cp + ci] = (uint16_t)lo;
 }
 
-// fp32 [Cout][Cin][KH][KW] -> split [Cout][2K]: k = (ky * KW + kx) * Cp + ci
+// fp32 [Cout][Cin][KH][KW] -> split chunk-major [Cout][K / 32][32 hi | 32 lo]: k = (ky * KW + kx) * Cp + ci
 // (per-tap channel runs padded to Cp), or with FLAT k = (ky * KW + kx) * Cin + ci
 // for k < KH * KW * Cin, zero up to K (the im2col operand's order)
 template <bool FLAT>
@@ -1389,8 +1403,9 @@ __global__ __launch_bounds__(256) void k_pack_weights(const float *__restrict__ 
     const float v = live ? w[(((int64_t)co * Cin + ci) * KH + ky) * KW + kx] : 0.f;
     uint32_t hi, lo;
     split2(v, hi, lo);
-    y[(int64_t)co * 2 * K + k] = (uint16_t)hi;
-    y[(int64_t)co * 2 * K + K + k] = (uint16_t)lo;
+    const int64_t yh = (int64_t)co * 2 * K + (DLS_W_CHUNKED ? (k / kBK) * 2 * kBK + k % kBK : k);
+    y[yh] = (uint16_t)hi;
+    y[yh + (DLS_W_CHUNKED ? kBK : K)] = (uint16_t)lo;
 }
 
 // im2col of an fp32 NCHW batch for a first layer with few input channels: split

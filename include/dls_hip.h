@@ -286,13 +286,14 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * bf16 pairs (hi = rne(x), lo = rne(x - hi)), products as hi*hi + hi*lo + lo*hi
  * with fp32 accumulation.
  * "split NHWC" activation: uint16 [B][H][W][2C] (per pixel C hi, then C lo).
- * split weights: uint16 [Cout][2K] (K hi, then K lo), k = (ky*KW + kx)*Cp + ci.
+ * split weights: uint16 [Cout][K/32][64], chunk-major: for each 32-wide chunk of
+ * k, 32 hi then 32 lo; k = (ky*KW + kx)*Cp + ci (K a multiple of 32).
  * dls_conv_pack_input_f32: NCHW fp32 [B][C][H][W] -> split NHWC with Cp channels
  * (Cp >= C, a multiple of 32; zeros beyond C).
  * dls_conv_pack_weights_f32: fp32 [Cout][Cin][KH][KW] -> split weights, Cp as above.
  * dls_conv_pack_im2col_f32 / dls_conv_pack_weights_im2col_f32: a first layer with
  * few input channels as a 1x1 convolution over its im2col: split NHWC
- * [B][Ho][Wo][2 Kp] / split weights [Cout][2 Kp], k = (ky*KW + kx)*C + ci, zero
+ * [B][Ho][Wo][2 Kp] / split weights [Cout][Kp/32][64], k = (ky*KW + kx)*C + ci, zero
  * for k >= KH*KW*C (Kp a multiple of 32).
  * dls_conv_bn_act_split: y = act(bn(conv(x, w)) [+ residual]) in split NHWC;
  * bn = the exact eval batch norm above (consts = [mean | iv | w | b], or null:
