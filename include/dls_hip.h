@@ -285,7 +285,8 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * same inputs give the same bits in any process.  fp32 values are carried as
  * bf16 pairs (hi = rne(x), lo = rne(x - hi)), products as hi*hi + hi*lo + lo*hi
  * with fp32 accumulation.
- * "split NHWC" activation: uint16 [B][H][W][2C] (per pixel C hi, then C lo).
+ * "split NHWC" activation: uint16 [B][H][W][C/32][64], chunk-major: per pixel and
+ * 32-channel chunk, 32 hi then 32 lo (C a multiple of 32).
  * split weights: uint16 [Cout][K/32][64], chunk-major: for each 32-wide chunk of
  * k, 32 hi then 32 lo; k = (ky*KW + kx)*Cp + ci (K a multiple of 32).
  * dls_conv_pack_input_f32: NCHW fp32 [B][C][H][W] -> split NHWC with Cp channels
@@ -303,7 +304,8 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * (KH*KW*C <= 32: a 3-channel 3x3 stem), straight from the fp32 NCHW image batch
  * (the im2col fused), w from dls_conv_pack_weights_im2col_f32 (Kp = 32).
  * dls_pool_linear_split: logits[b][o] = sum_c mean_pixels(x[b])[c] * weight[o][c]
- * + bias[o] over a split NHWC [B][HW][2C] activation (C <= 2048; bias may be
+ * + bias[o] over a split NHWC [B][HW][2C] activation (C <= 2048, a multiple of
+ * 32; bias may be
  * null), every sum in a fixed order. */
 int dls_conv_pack_input_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, int32_t Cp,
                             uint16_t *out, dls_stream_t stream);
