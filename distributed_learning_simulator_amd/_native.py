@@ -374,9 +374,8 @@ def bn_act_exact(x, consts, residual=None, relu=True, out=None, inplace=False, s
 
 # ------------------------------------------------ deterministic convolutions
 # "split" tensors (csrc/conv.hip): an fp32 value as a bf16 pair (hi, lo), stored
-# as int16 — activations [B, H, W, 2C] (chunk-major: per pixel and 32 channels,
-# 32 hi then 32 lo), weights [Cout, 2K] (chunk-major: per 32-wide chunk of k, 32
-# hi then 32 lo; k = (ky*KW + kx)*Cp + ci).
+# as int16 — activations [B, H, W, 2C] (per pixel C hi then C lo), weights
+# [Cout, 2K] (K hi then K lo, k = (ky*KW + kx)*Cp + ci).
 
 def _check_same_device(fn, x, **others):
     for name, t in others.items():
@@ -539,12 +538,9 @@ def pool_linear(x, weight, bias=None, stream=None):
     return out
 
 
-SPLIT_CHUNK = 32  # split tensors are chunk-major: per pixel, per 32 channels, 32 hi then 32 lo
-
-
 def split_to_f32(x):
     """hi + lo of a split NHWC tensor as fp32 NCHW (test / debugging helper)."""
     c = x.shape[-1] // 2
     u = x.to(torch.int32) & 0xFFFF
-    f = (u << 16).view(torch.float32).reshape(*x.shape[:-1], c // SPLIT_CHUNK, 2, SPLIT_CHUNK)
-    return (f[..., 0, :] + f[..., 1, :]).reshape(*x.shape[:-1], c).permute(0, 3, 1, 2).contiguous()
+    f = (u << 16).view(torch.float32)
+    return (f[..., :c] + f[..., c:]).permute(0, 3, 1, 2).contiguous()

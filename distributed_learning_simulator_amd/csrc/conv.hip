@@ -21,15 +21,10 @@
 // (tests/test_gpu_conv.py).
 //
 // Layouts (HBM):
-//   activations  "split NHWC": uint16 [B][H][W][C / 32][64], chunk-major: per
-//                pixel and 32-channel chunk, 32 bf16 hi then 32 bf16 lo (4 B per
-//                element, the size of the fp32 tensor), so a chunk's halo row
-//                is one 128-B line;
-//   weights      uint16 [Cout][K / 32][64], chunk-major: per output channel and
-//                32-wide chunk of k, 32 hi then 32 lo, k = (ky * KW + kx) * C + ci
-//                (C = the input's padded channels), so a step's 32-channel row
-//                piece is one 128-B line (K hi then K lo made it two half lines:
-//                -1.8 % per forward, profiles/r06_conv_wchunk_ab.txt).
+//   activations  "split NHWC": uint16 [B][H][W][2C], per pixel C bf16 hi then C
+//                bf16 lo (4 B per element, the size of the fp32 tensor);
+//   weights      uint16 [Cout][2K], per output channel K hi then K lo,
+//                k = (ky * KW + kx) * C + ci (C = the input's padded channels).
 // Implicit GEMM, D[co][pixel] = sum_k W[co][k] X[k][pixel]: A = weights (rows =
 // output channels), B = the input pixels' channel runs under a tap (zero outside
 // the image), so a lane's 16-element MFMA fragment is one 16-B piece of a
@@ -77,12 +72,6 @@
 #ifndef DLS_STEM_TILES  // probe knob: pixel tiles per block of the CIFAR stem (k_conv_stem, XT)
 #define DLS_STEM_TILES 4
 #endif
-#ifndef DLS_W_CHUNKED  // probe knob: 0 = split weights [Cout][K hi | K lo] (rounds 5-6); 1 = chunk-major (the ABI's)
-#define DLS_W_CHUNKED 1
-#endif
-#ifndef DLS_X_CHUNKED  // probe knob: 0 = split activations [pixel][C hi | C lo]; 1 = chunk-major (the ABI's)
-#define DLS_X_CHUNKED 1
-#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -129,7 +118,7 @@ __device__ __forceinline__ void split2x2(float a, float b, uint32_t &hi2, uint32
 
 struct ConvArgs {
     const uint16_t *x;      // split NHWC input [B][H][W][2C]
-    const uint16_t *w;      // split weights [Cout][K / 32][32 hi | 32 lo]
+    const uint16_t *w;      // split weights [Cout][2K]
     const float *consts;    // eval batch norm [mean | iv | w | b] x Cout, or null
     const uint16_t *res;    // split residual [B][Ho][Wo][2 Cout], or null
     uint16_t *y;            // split output [B][Ho][Wo][2 Cout]
@@ -141,24 +130,6 @@ struct ConvArgs {
 constexpr int kWaveTile = 64;  // a wave's output tile: 64 channels x 64 pixels
 constexpr int kBK = 32;        // channels per staged chunk
 constexpr int kRowB = 4 * kBK + 16;  // LDS row: kBK hi, kBK lo (bf16), 16 B pad
-
-// Offset (uint16 elements, within a pixel's 2C) of channel c's hi; its lo is
-// xlo(C) further (c's chunk: 32 hi then 32 lo when DLS_X_CHUNKED)
-__device__ __forceinline__ int xoff(int C, int c) { return DLS_X_CHUNKED ? 2 * (c & ~31) + (c & 31) : c; }
-__device__ __forceinline__ int xlo(int C) { return DLS_X_CHUNKED ? 32 : C; }
-// the 8 channels ci0 + 8 (part & 3) .. + 7 of the chunk at ci0, hi (part < 4) or lo
-__device__ __forceinline__ int xpiece(int C, int ci0, int part) {
-    if (DLS_X_CHUNKED) return 2 * ci0 + 8 * part;
-    return part < 4 ? ci0 + 8 * part : C + ci0 + 8 * (part - 4);
-}
-
-// Offset (uint16 elements, within an output channel's 2K) of the 8 weights
-// k0 .. k0 + 7 (k0 a multiple of 8) of chunk-relative piece `part` (0..3 hi,
-// 4..7 lo) of the chunk starting at kc (a multiple of kBK)
-__device__ __forceinline__ int woff(int K, int kc, int part) {
-    if (DLS_W_CHUNKED) return 2 * kc + 8 * part;
-    return part < 4 ? kc + 8 * part : K + kc + 8 * (part - 4);
-}
 
 typedef f32x16 WaveAcc[2][2];
 typedef f32x4 WaveAcc16[4][4];  // the same 64 x 64 tile as 4 x 4 tiles of 16 x 16
@@ -288,9 +259,9 @@ __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, cons
 #pragma unroll
             for (int u = 0; u < NPC; ++u) {
                 const int px = pix0 + (tid + NT * u) / GPP;
-                const int64_t ob = (int64_t)(px < a.M ? px : 0) * (2 * a.Cout) + xoff(a.Cout, co);
+                const int64_t ob = (int64_t)(px < a.M ? px : 0) * (2 * a.Cout) + co;
                 rpf[u][0] = *reinterpret_cast<const u32x4 *>(a.res + ob);
-                rpf[u][1] = *reinterpret_cast<const u32x4 *>(a.res + ob + xlo(a.Cout));
+                rpf[u][1] = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
             }
         }
         if (p > 0) __syncthreads();  // the previous pass's reads are done
@@ -323,7 +294,7 @@ __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, cons
             const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4);
             const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4 + 16);
             f32x2 v2[4] = {f32x2{v0[0], v0[1]}, f32x2{v0[2], v0[3]}, f32x2{v1[0], v1[1]}, f32x2{v1[2], v1[3]}};
-            const int64_t ob = (int64_t)px * (2 * a.Cout) + xoff(a.Cout, co);
+            const int64_t ob = (int64_t)px * (2 * a.Cout) + co;
             if (a.consts) {  // fma(w, (x - mean) * iv, b), element pairs on packed fp32
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v2[q] = __builtin_elementwise_fma(wv2[q], (v2[q] - m2[q]) * iv2[q], bv2[q]);
@@ -344,7 +315,7 @@ __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, cons
 #pragma unroll
             for (int q = 0; q < 4; ++q) split2x2(v[2 * q], v[2 * q + 1], hi[q], lo[q]);
             *reinterpret_cast<u32x4 *>(a.y + ob) = u32x4{hi[0], hi[1], hi[2], hi[3]};
-            *reinterpret_cast<u32x4 *>(a.y + ob + xlo(a.Cout)) = u32x4{lo[0], lo[1], lo[2], lo[3]};
+            *reinterpret_cast<u32x4 *>(a.y + ob + a.Cout) = u32x4{lo[0], lo[1], lo[2], lo[3]};
         }
     }
 }
@@ -426,10 +397,10 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
         const int tap = c / cchunks, ci0 = (c - tap * cchunks) * kBK;
         const int ky = tap / a.KW, kx = tap - ky * a.KW;
         const int kc = tap * a.C + ci0;
-        const int wo = woff(a.K, kc, part);
+        const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
 #pragma unroll
         for (int u = 0; u < NA; ++u) ra[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
-        const int xo = xpiece(a.C, ci0, part);
+        const int xo = part < HP ? ci0 + part * 8 : a.C + ci0 + (part - HP) * 8;
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
             const int iy = piy[u] + ky, ix = pix_[u] + kx;
@@ -562,7 +533,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
 
     u32x4 hreg[NHMAX], areg[NA];
     auto hload = [&](int cc) {
-        const int xo = xpiece(a.C, cc * BK, part);
+        const int xo = part < HP ? cc * BK + part * 8 : a.C + cc * BK + (part - HP) * 8;
 #pragma unroll
         for (int u = 0; u < NHMAX; ++u)
             hreg[u] = hpix[u] >= 0
@@ -577,7 +548,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     };
     auto aload = [&](int cc, int tap) {
         const int kc = tap * a.C + cc * BK;
-        const int wo = woff(a.K, kc, part);
+        const int wo = part < HP ? kc + part * 8 : a.K + kc + (part - HP) * 8;
 #pragma unroll
         for (int u = 0; u < NA; ++u) areg[u] = *reinterpret_cast<const u32x4 *>(wrow[u] + wo);
     };
@@ -750,19 +721,19 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     for (int u = 0; u < NAI; ++u) {
         const int row = 8 * (wv * NAI + u) + lr;
         const int p = sl ^ ((row >> 1) & 7);
-        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + woff(a.K, 0, p);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
     }
     auto issue_weights = [&](int step, int slot) {  // step's weights into ring slot slot % 3
         const int cc = step / 9, tap = step - 9 * cc;
         const int kc = tap * a.C + cc * kBK;
         uint8_t *dst = abuf0 + (slot % 3) * AB;
 #pragma unroll
-        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + (DLS_W_CHUNKED ? 2 * kc : kc), dst + (wv * NAI + u) * 8 * RB);
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
     };
     auto issue_halo = [&](int u, int cc) {
         const int v = hsrc[u], p = v & 7;
         const uint16_t *src =
-            v >= 0 ? a.x + (int64_t)(v >> 3) * (2 * a.C) + xpiece(a.C, cc * kBK, p) : zero;
+            v >= 0 ? a.x + (int64_t)(v >> 3) * (2 * a.C) + ((p & 4) ? a.C : 0) + 8 * (p & 3) + cc * kBK : zero;
         glds16(src, hbuf0 + (NHB == 2 ? (cc & 1) * HB : 0) + (u * NW + wv) * 8 * RB);
     };
 
@@ -950,7 +921,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe16(ConvArg
     for (int u = 0; u < NAI; ++u) {
         const int row = 8 * (wv * NAI + u) + lr;
         const int p = sl ^ (row & 7);
-        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + woff(a.K, 0, p);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
     }
     auto issue_weights = [&](int step, int slot) {
         const int cc = step / 9, tap = step - 9 * cc;
@@ -959,12 +930,12 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe16(ConvArg
         const int kc = tap * Cv + cc * kBK;
         uint8_t *dst = abuf0 + (slot % 3) * AB;
 #pragma unroll
-        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + (DLS_W_CHUNKED ? 2 * kc : kc), dst + (wv * NAI + u) * 8 * RB);
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
     };
     auto issue_halo = [&](int u, int cc) {
         const int v = hsrc[u], p = v & 7;
         const uint16_t *src =
-            v >= 0 ? a.x + (int64_t)(v >> 3) * (2 * a.C) + xpiece(a.C, cc * kBK, p) : zero;
+            v >= 0 ? a.x + (int64_t)(v >> 3) * (2 * a.C) + ((p & 4) ? a.C : 0) + 8 * (p & 3) + cc * kBK : zero;
         glds16(src, hbuf0 + (NHB == 2 ? (cc & 1) * HB : 0) + (u * NW + wv) * 8 * RB);
     };
 
@@ -1140,14 +1111,14 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs
     for (int u = 0; u < NAI; ++u) {
         const int row = 8 * (wv * NAI + u) + lr;
         const int p = sl ^ ((row >> 1) & 7);
-        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + woff(a.K, 0, p);
+        asrc[u] = a.w + (int64_t)(co0 + row) * (2 * a.K) + ((p & 4) ? a.K : 0) + 8 * (p & 3);
     }
     auto issue_weights = [&](int step, int slot) {
         const int cc = step / 9, tap = kPhaseTap[step - 9 * cc];
         const int kc = tap * a.C + cc * kBK;
         uint8_t *dst = abuf0 + (slot % 3) * AB;
 #pragma unroll
-        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + (DLS_W_CHUNKED ? 2 * kc : kc), dst + (wv * NAI + u) * 8 * RB);
+        for (int u = 0; u < NAI; ++u) glds16(asrc[u] + kc, dst + (wv * NAI + u) * 8 * RB);
     };
     // phase g = 4 cc + p (p: 0 = (1,1), 1 = (1,0), 2 = (0,1), 3 = (0,0)) into buffer g & 1
     auto issue_halo = [&](int g) {
@@ -1157,7 +1128,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs
         for (int u = 0; u < NHI; ++u) {
             const int v = hpix[u], pc = hpc[u];
             const uint16_t *src =
-                v >= 0 ? a.x + (int64_t)(v - back) * (2 * a.C) + xpiece(a.C, cc * kBK, pc)
+                v >= 0 ? a.x + (int64_t)(v - back) * (2 * a.C) + ((pc & 4) ? a.C : 0) + 8 * (pc & 3) + cc * kBK
                        : zero;
             glds16(src, hbuf0 + (g & 1) * HB + (u * NW + wv) * 8 * RB);
         }
@@ -1397,11 +1368,11 @@ __global__ __launch_bounds__(256) void k_pack_input(const float *__restrict__ x,
     const float v = ci < C ? x[(b * C + ci) * HW + s] : 0.f;
     uint32_t hi, lo;
     split2(v, hi, lo);
-    y[pix * 2 * Cp + xoff(Cp, ci)] = (uint16_t)hi;
-    y[pix * 2 * Cp + xoff(Cp, ci) + xlo(Cp)] = (uint16_t)lo;
+    y[pix * 2 * Cp + ci] = (uint16_t)hi;
+    y[pix * 2 * Cp + Cp + ci] = (uint16_t)lo;
 }
 
-// fp32 [Cout][Cin][KH][KW] -> split chunk-major [Cout][K / 32][32 hi | 32 lo]: k = (ky * KW + kx) * Cp + ci
+// fp32 [Cout][Cin][KH][KW] -> split [Cout][2K]: k = (ky * KW + kx) * Cp + ci
 // (per-tap channel runs padded to Cp), or with FLAT k = (ky * KW + kx) * Cin + ci
 // for k < KH * KW * Cin, zero up to K (the im2col operand's order)
 template <bool FLAT>
@@ -1418,9 +1389,8 @@ __global__ __launch_bounds__(256) void k_pack_weights(const float *__restrict__ 
     const float v = live ? w[(((int64_t)co * Cin + ci) * KH + ky) * KW + kx] : 0.f;
     uint32_t hi, lo;
     split2(v, hi, lo);
-    const int64_t yh = (int64_t)co * 2 * K + (DLS_W_CHUNKED ? (k / kBK) * 2 * kBK + k % kBK : k);
-    y[yh] = (uint16_t)hi;
-    y[yh + (DLS_W_CHUNKED ? kBK : K)] = (uint16_t)lo;
+    y[(int64_t)co * 2 * K + k] = (uint16_t)hi;
+    y[(int64_t)co * 2 * K + K + k] = (uint16_t)lo;
 }
 
 // im2col of an fp32 NCHW batch for a first layer with few input channels: split
@@ -1446,8 +1416,8 @@ __global__ __launch_bounds__(256) void k_pack_im2col(const float *__restrict__ x
         v = x[((b * C + ci) * H + iy) * W + ix];
     uint32_t hi, lo;
     split2(v, hi, lo);
-    y[pix * 2 * Kp + xoff(Kp, k)] = (uint16_t)hi;
-    y[pix * 2 * Kp + xoff(Kp, k) + xlo(Kp)] = (uint16_t)lo;
+    y[pix * 2 * Kp + k] = (uint16_t)hi;
+    y[pix * 2 * Kp + Kp + k] = (uint16_t)lo;
 }
 
 // Global average pool + linear layer over split NHWC [B][HW][2C]: one block per
@@ -1466,8 +1436,7 @@ __global__ __launch_bounds__(kPoolBlock) void k_pool_linear(const uint16_t *__re
     for (int c = tid; c < C; c += kPoolBlock) {
         float s = 0.f;
         for (int q = 0; q < HW; ++q)
-            s += bf16_to_f32(xb[(int64_t)q * 2 * C + xoff(C, c)]) +
-                 bf16_to_f32(xb[(int64_t)q * 2 * C + xoff(C, c) + xlo(C)]);
+            s += bf16_to_f32(xb[(int64_t)q * 2 * C + c]) + bf16_to_f32(xb[(int64_t)q * 2 * C + C + c]);
         feat[c] = s * inv;
     }
     __syncthreads();
@@ -1771,9 +1740,8 @@ int dls_conv_stem_bn_act_f32(const float *x, int64_t B, int32_t C, int32_t H, in
 int dls_pool_linear_split(const uint16_t *x, int64_t B, int32_t HW, int32_t C, const float *weight,
                           const float *bias, int32_t O, float *out, dls_stream_t stream) {
     DLS_REQUIRE(x && weight && out, DLS_EINVAL, "dls_pool_linear_split: null pointer");
-    DLS_REQUIRE(B >= 0 && HW > 0 && C > 0 && C <= 2048 && C % 32 == 0 && O > 0, DLS_EINVAL,
-                "dls_pool_linear_split: B=%lld HW=%d C=%d O=%d (C <= 2048, a multiple of 32)", (long long)B, HW,
-                C, O);
+    DLS_REQUIRE(B >= 0 && HW > 0 && C > 0 && C <= 2048 && O > 0, DLS_EINVAL,
+                "dls_pool_linear_split: B=%lld HW=%d C=%d O=%d (C <= 2048)", (long long)B, HW, C, O);
     if (B == 0) return DLS_OK;
     hipLaunchKernelGGL(k_pool_linear, dim3((unsigned)B), dim3(kPoolBlock), 0, as_stream(stream), x,
                        (int)HW, (int)C, weight, bias, (int)O, out);

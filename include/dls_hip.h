@@ -285,16 +285,14 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * same inputs give the same bits in any process.  fp32 values are carried as
  * bf16 pairs (hi = rne(x), lo = rne(x - hi)), products as hi*hi + hi*lo + lo*hi
  * with fp32 accumulation.
- * "split NHWC" activation: uint16 [B][H][W][C/32][64], chunk-major: per pixel and
- * 32-channel chunk, 32 hi then 32 lo (C a multiple of 32).
- * split weights: uint16 [Cout][K/32][64], chunk-major: for each 32-wide chunk of
- * k, 32 hi then 32 lo; k = (ky*KW + kx)*Cp + ci (K a multiple of 32).
+ * "split NHWC" activation: uint16 [B][H][W][2C] (per pixel C hi, then C lo).
+ * split weights: uint16 [Cout][2K] (K hi, then K lo), k = (ky*KW + kx)*Cp + ci.
  * dls_conv_pack_input_f32: NCHW fp32 [B][C][H][W] -> split NHWC with Cp channels
  * (Cp >= C, a multiple of 32; zeros beyond C).
  * dls_conv_pack_weights_f32: fp32 [Cout][Cin][KH][KW] -> split weights, Cp as above.
  * dls_conv_pack_im2col_f32 / dls_conv_pack_weights_im2col_f32: a first layer with
  * few input channels as a 1x1 convolution over its im2col: split NHWC
- * [B][Ho][Wo][2 Kp] / split weights [Cout][Kp/32][64], k = (ky*KW + kx)*C + ci, zero
+ * [B][Ho][Wo][2 Kp] / split weights [Cout][2 Kp], k = (ky*KW + kx)*C + ci, zero
  * for k >= KH*KW*C (Kp a multiple of 32).
  * dls_conv_bn_act_split: y = act(bn(conv(x, w)) [+ residual]) in split NHWC;
  * bn = the exact eval batch norm above (consts = [mean | iv | w | b], or null:
@@ -304,8 +302,7 @@ int dls_bn_act_exact_nchw_f32(const float *x, int64_t N, int32_t C, int64_t HW,
  * (KH*KW*C <= 32: a 3-channel 3x3 stem), straight from the fp32 NCHW image batch
  * (the im2col fused), w from dls_conv_pack_weights_im2col_f32 (Kp = 32).
  * dls_pool_linear_split: logits[b][o] = sum_c mean_pixels(x[b])[c] * weight[o][c]
- * + bias[o] over a split NHWC [B][HW][2C] activation (C <= 2048, a multiple of
- * 32; bias may be
+ * + bias[o] over a split NHWC [B][HW][2C] activation (C <= 2048; bias may be
  * null), every sum in a fixed order. */
 int dls_conv_pack_input_f32(const float *x, int64_t B, int32_t C, int32_t H, int32_t W, int32_t Cp,
                             uint16_t *out, dls_stream_t stream);
