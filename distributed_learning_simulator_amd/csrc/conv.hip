@@ -34,7 +34,7 @@
 // ds_read_b128 fragments).  Kernels:
 //   k_conv3x3_pipe16  3x3 stride-1 convolutions (the default): k_conv3x3_pipe's
 //                   pipeline on v_mfma_f32_16x16x32_bf16 (4 x 4 tiles of 16 x 16
-//                   per wave; -2 % per forward, profiles/r06_conv_mf16_ab.txt);
+//                   per wave; -0.9 % per forward, profiles/r06_forward_mf16_ab.txt);
 //   k_conv3x3_pipe  3x3 stride-1 convolutions: the block's pixels are whole
 //                   output rows, so its input is ONE halo tile staged once per
 //                   channel chunk and read by all 9 taps at shifted rows; every
