@@ -57,6 +57,8 @@
 // profiles/r05_conv_probe.txt, DESIGN.md §4.
 #include "dls_common.h"
 
+#include <mutex>
+
 #ifndef DLS_CONV_GENERIC_ONLY
 #define DLS_CONV_GENERIC_ONLY 0
 #endif
@@ -71,6 +73,9 @@
 #endif
 #ifndef DLS_STEM_TILES  // probe knob: pixel tiles per block of the CIFAR stem (k_conv_stem, XT)
 #define DLS_STEM_TILES 4
+#endif
+#ifndef DLS_CONV_SERPENTINE  // probe knob: 0 = every launch walks its tiles forward
+#define DLS_CONV_SERPENTINE 1
 #endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
@@ -125,6 +130,7 @@ struct ConvArgs {
     int H, W, C, Ho, Wo, Cout, KW, taps, stride, pad, K, M, relu;
     int pix_tiles, co_tiles;
     int B, TI, TR, NH;  // halo kernel: images / rows per pixel tile, halo rows
+    int rev;            // 1: each XCD walks its tile run backwards (tile_of_block)
 };
 
 constexpr int kWaveTile = 64;  // a wave's output tile: 64 channels x 64 pixels
@@ -325,12 +331,17 @@ __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, cons
 // holds ceil((nblk - x) / 8) blocks), (pixel tile, channel tile) pairs with the
 // channel tile fastest, so blocks reading the same input pixels share an L2.
 // (Channel tile slowest instead, so an XCD's blocks share weights: null,
-// profiles/r06_conv_ab.txt.)
-__device__ __forceinline__ void tile_of_block(int co_tiles, int &co_t, int &pix_t) {
+// profiles/r06_conv_ab.txt.)  rev: each XCD walks its run from the end, so a
+// layer whose input was written forwards starts on the pixels written last (still
+// in the Infinity Cache); the host alternates it along the forward
+// (conv_walk_direction).  The order of the tiles never changes any output's bits.
+__device__ __forceinline__ void tile_of_block(int co_tiles, int &co_t, int &pix_t, int rev) {
     const int nblk = gridDim.x, bid = blockIdx.x, x = bid & 7;
     // blocks on XCDs 0..x-1: sum of ceil((nblk - j) / 8)
     const int q = nblk >> 3, rmd = nblk & 7;
-    const int t = x * q + (x < rmd ? x : rmd) + (bid >> 3);
+    const int cnt = q + (x < rmd ? 1 : 0);  // blocks on XCD x
+    const int k = rev ? cnt - 1 - (bid >> 3) : (bid >> 3);
+    const int t = x * q + (x < rmd ? x : rmd) + k;
     co_t = t % co_tiles;
     pix_t = t / co_tiles;
 }
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX) void k_conv_bf16x3(ConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
     int co_t, pix_t;
-    tile_of_block(a.co_tiles, co_t, pix_t);
+    tile_of_block(a.co_tiles, co_t, pix_t, a.rev);
     const int co0 = co_t * BMC;
     const int pix0 = pix_t * BNP;
 
@@ -494,7 +505,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 2) void k_conv3x3_halo(ConvArgs a)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = wid / WPIX, wp = wid % WPIX;
     int co_t, pt;
-    tile_of_block(a.co_tiles, co_t, pt);
+    tile_of_block(a.co_tiles, co_t, pt, a.rev);
     const int co0 = co_t * BMC;
     const int pix0 = pt * BNP;
     const int W = a.W, H = a.H, W2 = W + 2;
@@ -677,7 +688,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe(ConvArgs 
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wc = wv / WPIX, wp = wv % WPIX;
     int co_t, pt;
-    tile_of_block(a.co_tiles, co_t, pt);
+    tile_of_block(a.co_tiles, co_t, pt, a.rev);
     const int co0 = co_t * BMC;
     const int pix0 = pt * BNP;
     const int W = a.W, H = a.H, TR = a.TR;
@@ -883,7 +894,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, OCC) void k_conv3x3_pipe16(ConvArg
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wc = wv / WPIX, wp = wv % WPIX;
     int co_t, pt;
-    tile_of_block(a.co_tiles, co_t, pt);
+    tile_of_block(a.co_tiles, co_t, pt, a.rev);
     const int co0 = co_t * BMC;
     const int pix0 = pt * BNP;
     const int W = a.W, H = a.H, TR = a.TR;
@@ -1070,7 +1081,7 @@ __global__ __launch_bounds__(64 * WCO * WPIX, 1) void k_conv3x3s2_phase(ConvArgs
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int wc = wv / WPIX, wp = wv % WPIX;
     int co_t, pt;
-    tile_of_block(a.co_tiles, co_t, pt);
+    tile_of_block(a.co_tiles, co_t, pt, a.rev);
     const int co0 = co_t * BMC;
     const int pix0 = pt * BNP;
     const int H = a.H, W = a.W, Ho = a.Ho, Wo = a.Wo, TR = a.TR;
@@ -1256,7 +1267,7 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
     const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
     const int r = lane & 31, h = lane >> 5;
     int co_t, pix_t;
-    tile_of_block(a.co_tiles, co_t, pix_t);
+    tile_of_block(a.co_tiles, co_t, pix_t, a.rev);
     const int co0 = co_t * kWaveTile;
     // the window rows oy0 - 1 .. oy0 + 8 of a tile's image, 8 columns x 4 per thread
     auto load_window = [&](int p0) {
@@ -1576,6 +1587,38 @@ int try_launch_pipe(ConvArgs a, hipStream_t st, int &rc) {
     return 1;
 }
 
+// The walk direction of a launch: the opposite of the one its input was
+// written in (a launch records its output's), forwards for an input no recent
+// launch wrote.  Performance only: no output depends on it.
+struct WalkMemo {
+    std::mutex m;
+    const void *ptr[16] = {};
+    int dir[16] = {};
+    int next = 0;
+};
+WalkMemo g_walk;
+
+int conv_walk_direction(const void *x) {
+    if (!DLS_CONV_SERPENTINE) return 0;
+    std::lock_guard<std::mutex> g(g_walk.m);
+    for (int i = 0; i < 16; ++i)
+        if (g_walk.ptr[i] == x) return !g_walk.dir[i];
+    return 0;
+}
+
+void conv_record_walk(const void *y, int dir) {
+    if (!DLS_CONV_SERPENTINE) return;
+    std::lock_guard<std::mutex> g(g_walk.m);
+    for (int i = 0; i < 16; ++i)
+        if (g_walk.ptr[i] == y) {
+            g_walk.dir[i] = dir;
+            return;
+        }
+    g_walk.ptr[g_walk.next] = y;
+    g_walk.dir[g_walk.next] = dir;
+    g_walk.next = (g_walk.next + 1) & 15;
+}
+
 }  // namespace
 }  // namespace dls
 
@@ -1665,6 +1708,8 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     ConvArgs a{x, w, consts, residual, y, (int)H, (int)W, (int)C, Ho, Wo, (int)Cout, (int)KW,
                (int)(KH * KW), (int)stride, (int)pad, (int)(KH * KW * C), (int)M, relu ? 1 : 0, 0, 0,
                (int)B, 0, 0, 0};
+    a.rev = conv_walk_direction(x);
+    conv_record_walk(y, a.rev);
     hipStream_t st = as_stream(stream);
     const bool wide = Cout % 128 == 0;
     // The kernel choice is a function of the shape alone (never of the process's
@@ -1718,6 +1763,7 @@ int dls_conv_stem_bn_act_f32(const float *x, int64_t B, int32_t C, int32_t H, in
     constexpr int WPIX = 4;
     ConvArgs a{nullptr, w, consts, nullptr, y, (int)H, (int)W, (int)C, Ho, Wo, (int)Cout, (int)KW,
                (int)(KH * KW), (int)stride, (int)pad, kBK, (int)M, relu ? 1 : 0, 0, 0, (int)B, 0, 0, 0};
+    conv_record_walk(y, 0);  // the stem walks forwards; the next layer backwards
     a.pix_tiles = (int)((M + kWaveTile * WPIX - 1) / (kWaveTile * WPIX));
     a.co_tiles = Cout / kWaveTile;
     const int64_t blocks = (int64_t)a.pix_tiles * a.co_tiles;
