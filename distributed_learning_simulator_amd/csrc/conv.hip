@@ -77,6 +77,9 @@
 #ifndef DLS_CONV_SERPENTINE  // probe knob: 0 = every launch walks its tiles forward
 #define DLS_CONV_SERPENTINE 1
 #endif
+#ifndef DLS_PIPE_NARROW  // probe knob: bit 0/1/2 = 128-channel-multiple layers 16/8/4 wide in 64-channel 4-wave blocks
+#define DLS_PIPE_NARROW 1  // 16 wide: -0.9 % per forward; 8 wide: null; 4 wide: +0.6 % (profiles/r06_forward_narrow_ab.txt)
+#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -1719,10 +1722,16 @@ int dls_conv_bn_act_split(const uint16_t *x, int64_t B, int32_t H, int32_t W, in
     if (!DLS_CONV_GENERIC_ONLY && KH == 3 && KW == 3 && stride == 1 && pad == 1) {
         int rc = DLS_OK;
         // the LDS-DMA pipelines (profiles/r06_conv_pipe_ab.txt): 128-channel
-        // multiples in 4-wave one-halo-buffer blocks two per CU on images at
-        // least 16 wide (16x16: -1 to -2 %; 8x8: +0.5 to +1.4 %), else in 8-wave
-        // double-buffered ones (8x8, 4x4); 64 channels in 4-wave one-halo-buffer
-        // blocks (32x32)
+        // multiples 16 wide in 64-channel 4-wave blocks of one whole 16x16 image
+        // (no halo rows re-read, half the weight bytes per MFMA), else in
+        // 128-channel 4-wave one-halo-buffer blocks two per CU on images at least
+        // 16 wide, else in 8-wave double-buffered ones (8x8, 4x4); 64 channels in
+        // 4-wave one-halo-buffer blocks (32x32)
+        const bool narrow = (W == 16 && (DLS_PIPE_NARROW & 1)) || (W == 8 && (DLS_PIPE_NARROW & 2)) ||
+                            (W == 4 && (DLS_PIPE_NARROW & 4));
+        if (DLS_CONV_PIPE && narrow &&
+            (try_launch_pipe<1, 4, 10, 1, 2>(a, st, rc) || try_launch_pipe<1, 4, 12, 1, 2>(a, st, rc)))
+            return rc;
         if (DLS_CONV_PIPE && wide &&
             ((W >= 16 && try_launch_pipe<2, 2, 5, 1, 2>(a, st, rc)) || try_launch_pipe<2, 4, 5>(a, st, rc) ||
              try_launch_pipe<2, 4, 6>(a, st, rc)))
