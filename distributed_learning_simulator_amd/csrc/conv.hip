@@ -80,6 +80,9 @@
 #ifndef DLS_PIPE_NARROW  // probe knob: bit 0/1/2 = 128-channel-multiple layers 16/8/4 wide in 64-channel 4-wave blocks
 #define DLS_PIPE_NARROW 1  // 16 wide: -0.9 % per forward; 8 wide: null; 4 wide: +0.6 % (profiles/r06_forward_narrow_ab.txt)
 #endif
+#ifndef DLS_STEM_PIXSPLIT  // probe knob: 1 = the stem's two epilogue passes split the pixels, not the channels
+#define DLS_STEM_PIXSPLIT 1
+#endif
 #ifndef DLS_CONV_PIPE  // probe knob: 0 = no LDS-DMA pipeline (k_conv3x3_halo for every 3x3 stride-1 shape)
 #define DLS_CONV_PIPE 1
 #endif
@@ -246,20 +249,26 @@ __device__ __forceinline__ void acc_to_lds(const WaveAcc16 &acc, uint8_t *smem, 
         }
 }
 
-template <int BMC, int BNP, int NT, int NPASS = 1, class Acc = WaveAcc>
+// PSPLIT (NPASS = 2, one channel tile): the passes split the pixels instead —
+// pass p transposes the waves whose pixels lie in its half, every channel — so
+// each pass stores whole 128-B runs of a pixel's hi (or lo) channels.
+template <int BMC, int BNP, int NT, int NPASS = 1, class Acc = WaveAcc, bool PSPLIT = false>
 __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, const ConvArgs &a,
                                              int co0, int pix0, int wc, int wp, int tid) {
     static_assert(NPASS == 1 || NPASS == 2, "epilogue passes");
-    constexpr int SLAB = BMC / NPASS;  // channels per pass
+    static_assert(!PSPLIT || (NPASS == 2 && BMC == kWaveTile && BNP % (2 * kWaveTile) == 0), "pixel passes");
+    constexpr int SLAB = PSPLIT ? BMC : BMC / NPASS;  // channels per pass
+    constexpr int PPP = PSPLIT ? BNP / NPASS : BNP;   // pixels per pass
     constexpr int EROW = 4 * SLAB + 16;
     constexpr int GPP = SLAB / 8;      // 8-channel groups per pixel
-    constexpr int NPC = BNP * GPP / NT;
-    static_assert(NT % GPP == 0 && (BNP * GPP) % NT == 0, "epilogue shape");
+    constexpr int NPC = PPP * GPP / NT;
+    static_assert(NT % GPP == 0 && (PPP * GPP) % NT == 0, "epilogue shape");
     const int lane = tid & 63;
     const int lc = 8 * (tid % GPP);  // a thread's channel group is fixed per pass
 #pragma unroll
     for (int p = 0; p < NPASS; ++p) {
-        const int co = co0 + (NPASS == 1 ? lc : (lc / 32) * kWaveTile + 32 * p + lc % 32);
+        const int co = co0 + (NPASS == 1 || PSPLIT ? lc : (lc / 32) * kWaveTile + 32 * p + lc % 32);
+        const int pp0 = pix0 + (PSPLIT ? p * PPP : 0);  // the pass's first pixel
         // the pass's residual pieces are loaded before the transpose, their
         // latency behind its LDS writes and barrier (-1 to -2 % on the residual
         // layers, profiles/r06_conv_ab.txt)
@@ -267,14 +276,19 @@ __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, cons
         if (a.res) {
 #pragma unroll
             for (int u = 0; u < NPC; ++u) {
-                const int px = pix0 + (tid + NT * u) / GPP;
+                const int px = pp0 + (tid + NT * u) / GPP;
                 const int64_t ob = (int64_t)(px < a.M ? px : 0) * (2 * a.Cout) + co;
                 rpf[u][0] = *reinterpret_cast<const u32x4 *>(a.res + ob);
                 rpf[u][1] = *reinterpret_cast<const u32x4 *>(a.res + ob + a.Cout);
             }
         }
         if (p > 0) __syncthreads();  // the previous pass's reads are done
-        acc_to_lds<NPASS, EROW>(acc, smem, wc, wp, lane, p);
+        if constexpr (PSPLIT) {
+            if (wp * kWaveTile / PPP == p)  // this wave's pixels are the pass's: rows wp*64 - p*PPP ..
+                acc_to_lds<1, EROW>(acc, smem - (ptrdiff_t)p * PPP * EROW, wc, wp, lane, 0);
+        } else {
+            acc_to_lds<NPASS, EROW>(acc, smem, wc, wp, lane, p);
+        }
         __syncthreads();
         // the 8 channels' batch-norm constants as element pairs: 8 vector loads
         f32x2 m2[4], iv2[4], wv2[4], bv2[4];
@@ -298,7 +312,7 @@ __device__ __forceinline__ void epilogue_lds(const Acc &acc, uint8_t *smem, cons
 #pragma unroll
         for (int u = 0; u < NPC; ++u) {
             const int pl = (tid + NT * u) / GPP;
-            const int px = pix0 + pl;
+            const int px = pp0 + pl;
             if (px >= a.M) continue;
             const f32x4 v0 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4);
             const f32x4 v1 = *reinterpret_cast<const f32x4 *>(smem + pl * EROW + lc * 4 + 16);
@@ -1367,7 +1381,7 @@ __global__ __launch_bounds__(64 * WPIX) void k_conv_stem(ConvArgs a, const float
         mfma_frag(acc, f[s]);
     }
     __syncthreads();  // the epilogue reuses the operands' LDS
-    epilogue_lds<kWaveTile, BNP, NT, 2>(acc, smem, a, co0, pix0, 0, wp, tid);
+    epilogue_lds<kWaveTile, BNP, NT, 2, WaveAcc, DLS_STEM_PIXSPLIT>(acc, smem, a, co0, pix0, 0, wp, tid);
     }
 }
 
