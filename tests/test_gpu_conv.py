@@ -382,3 +382,21 @@ def test_queued_evaluations_on_several_streams_equal_one_stream():
             for c in coal]
     assert out[2] == sync
     assert len(set(out[2])) > 2  # the coalitions' models differ
+
+
+@pytest.mark.parametrize("cin,cout,s,H", [(64, 64, 1, 32), (128, 128, 1, 16), (256, 256, 1, 8), (64, 128, 2, 32)])
+def test_walk_direction_does_not_change_bits(cin, cout, s, H):
+    """A launch whose input is a recent launch's output walks its tiles the other
+    way (the serpentine walk, csrc/conv.hip conv_walk_direction); a fresh copy of
+    the same input walks forwards.  Both give the same bits (no output's
+    reduction order depends on the tile order)."""
+    from distributed_learning_simulator_amd import _native
+    _, (xs, ws, geom, consts, rs), _ = _run(cin, cin, 3, 1, H, H, False, 5, seed=21)
+    g = torch.Generator().manual_seed(22)
+    w2 = (torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5).to(dev)
+    ws2 = _native.conv_pack_weights(w2)
+    h = _native.conv_bn_act(xs, ws, *geom, consts, None, relu=True)  # h recorded as written forwards
+    walked = _native.conv_bn_act(h, ws2, (3, 3), s, 1, None, None, relu=True)  # reads h: backwards
+    fresh = _native.conv_bn_act(h.clone(), ws2, (3, 3), s, 1, None, None, relu=True)  # forwards
+    torch.cuda.synchronize()
+    assert torch.equal(walked, fresh)
