@@ -47,7 +47,12 @@
 //                   the input's row / column parity images, on the same
 //                   pipeline (each input pixel staged once per channel chunk);
 //   k_conv_bf16x3   anything else (1x1, sizes the tilings do not fit): every
-//                   (tap, chunk) gathers its B tile.
+//                   (tap, chunk) gathers its B tile;
+//   k_conv_stem     the 3-channel 3x3 stem with its im2col fused (a block walks 4
+//                   pixel tiles; its epilogue passes split the pixels).
+// Every launch walks its XCDs' tile runs forwards or backwards — the opposite of
+// the direction its input was written in (conv_walk_direction), so a layer starts
+// on what the previous one wrote last; no output depends on the order.
 // The epilogue goes through LDS: the raw tile is transposed to [pixel][channel]
 // and each thread applies the eval batch norm with the batch-norm library's
 // arithmetic (infer.hip, k_bn_act_exact: fma(w, (x - mean) * iv, b)), the
