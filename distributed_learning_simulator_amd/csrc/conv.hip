@@ -48,7 +48,7 @@
 //                   pipeline (each input pixel staged once per channel chunk);
 //   k_conv_bf16x3   anything else (1x1, sizes the tilings do not fit): every
 //                   (tap, chunk) gathers its B tile;
-//   k_conv_stem     the 3-channel 3x3 stem with its im2col fused (a block walks 4
+//   k_conv_stem     the 3-channel 3x3 stem with its im2col fused (a block walks 2
 //                   pixel tiles; its epilogue passes split the pixels).
 // Every launch walks its XCDs' tile runs forwards or backwards — the opposite of
 // the direction its input was written in (conv_walk_direction), so a layer starts
@@ -77,7 +77,7 @@
 #define DLS_CONV_MF16 1
 #endif
 #ifndef DLS_STEM_TILES  // probe knob: pixel tiles per block of the CIFAR stem (k_conv_stem, XT)
-#define DLS_STEM_TILES 4
+#define DLS_STEM_TILES 2
 #endif
 #ifndef DLS_CONV_SERPENTINE  // probe knob: 0 = every launch walks its tiles forward
 #define DLS_CONV_SERPENTINE 1
